@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py — Raft group-steps/sec of the MI355X batched Raft engine.
+
+Workload (BASELINE.json configs[2], "config 3"): 10^6 five-replica groups per
+GPU, seeded 5% message drop, leader-isolation churn (1e-3 per group-step, 15
+steps), one client command per group-step with probability 1/4.  A "step" is
+one lockstep heartbeat period of every group: timers, the
+RequestVote phase, the AppendEntries/commit phase and client commands, with
+all state resident in HBM before the timed region starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Multi-GPU: one process per GPU, each owns its own contiguous range of global
+group ids (weak scaling; no data-path collective).  The per-step global
+counters (commits, leaders, safety flags, ...) are all-reduced over RCCL in
+batches on a side stream.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+abi = importlib.import_module("raft-kotlin_amd.abi")
+
+METRIC = "Raft group-steps/sec (whole node) at 1M×5-replica groups; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+STATE_BYTES_PER_REPLICA = 4 * abi.NUM_FIELDS
+GROUP_EXTRA_BYTES = 4 * abi.GROUP_EXTRA
+
+
+def algorithmic_bytes(c: np.ndarray, G: int, R: int, launches: int) -> float:
+    """Algorithmic HBM bytes of the step kernel over the counted steps
+    (DESIGN.md §4): the group state is read and written once per launch, an
+    active leader session (2R int32) once per launch, and every log slot the
+    handlers touch once (4 B per term read, 8 B per entry read/write)."""
+    ix = abi.C_INDEX
+    state = 2.0 * G * (R * STATE_BYTES_PER_REPLICA + GROUP_EXTRA_BYTES) * launches
+    steps = max(1, c.shape[0])
+    sessions = 2.0 * 8 * R * (c[:, ix["sessions_ticked"]].sum() / steps) * launches
+    log = (4.0 * c[:, ix["prev_reads_leader"]].sum() + 8.0 * c[:, ix["entry_reads_leader"]].sum()
+           + 4.0 * c[:, ix["prev_reads_follower"]].sum() + 8.0 * c[:, ix["entry_writes"]].sum()
+           + 4.0 * c[:, ix["vote_log_reads"]].sum() + 8.0 * c[:, ix["commands"]].sum())
+    return state + sessions + log
+
+
+def cpu_baseline(args, kw, log_cap):
+    """Oracle (scalar C restatement of the reference) on a bounded sample of
+    the same workload, on this host's cores (rank 0, N=1 only)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    G = args.cpu_groups
+    o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
+    o.step(args.warmup_cpu, nthreads=threads, counters=False)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        o.step(args.cpu_chunk, nthreads=threads, counters=True)
+        n += args.cpu_chunk
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": G * n / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/raft_oracle.c, {G} groups x {n} steps of the same config "
+                      f"(after {args.warmup_cpu} warmup steps), {dt:.1f} s, pthreads over groups"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10_000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--steps-per-launch", type=int, default=0)
+    ap.add_argument("--log-cap", type=int, default=0)
+    ap.add_argument("--reduce-every", type=int, default=256, help="steps per counter all-reduce")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-groups", type=int, default=20_000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-chunk", type=int, default=20)
+    ap.add_argument("--warmup-cpu", type=int, default=40)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    eng_mod = importlib.import_module("raft-kotlin_amd.engine")
+    kw = dict(abi.CONFIGS[args.config])
+    R = kw["R"]
+    if args.scaling == "weak":
+        G_local = args.groups
+        g0 = rank * G_local
+    else:
+        G_local = args.groups // world + (1 if rank < args.groups % world else 0)
+        g0 = rank * (args.groups // world) + min(rank, args.groups % world)
+    total_steps = args.warmup + args.steps
+    log_cap = args.log_cap or int(64 + 0.3 * total_steps)
+    spl = args.steps_per_launch
+    params = abi.make_params(log_cap=log_cap, steps_per_launch=spl, **dict(kw, G=G_local, g0=g0))
+    eng = eng_mod.RaftEngine(params, device=local)
+    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
+    counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+    wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+
+    # ---- warmup (untimed) ----
+    if args.warmup:
+        eng.step_async(args.warmup, wcount.data_ptr())
+    eng.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+
+    # ---- timed region ----
+    comm_stream = torch.cuda.Stream(device=dev)
+    eng.set_kernel_timing(True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    done = 0
+    while done < args.steps:
+        k = min(args.reduce_every, args.steps - done)
+        eng.step_async(k, counters[done].data_ptr())
+        if world > 1:
+            # the only collective: the batched per-step counter all-reduce,
+            # off the critical path on a side stream (counters never feed back)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            comm_stream.wait_event(ev)
+            with torch.cuda.stream(comm_stream):
+                dist.all_reduce(counters[done:done + k])
+        done += k
+    ev1.record(stream)
+    eng.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    kern_ms, launches = eng.kernel_time()
+    eng.set_kernel_timing(False)
+
+    elapsed = max(wall, ev_ms / 1e3)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    c_all = counters.cpu().numpy()[:, : abi.NUM_COUNTERS]     # already global if world > 1
+    local_counts = None
+    if world == 1:
+        local_counts = c_all
+    total_groups = G_local * world if args.scaling == "weak" else args.groups
+    value = total_groups * args.steps / elapsed
+
+    # roofline of the dominant kernel (step_kernel), from this rank's counters
+    if world > 1:
+        # the all-reduced counters are global; scale to this rank's share
+        local_counts = c_all * (G_local / total_groups)
+    bytes_alg = algorithmic_bytes(local_counts, G_local, R, launches)
+    kern_avg_ms = kern_ms / max(1, launches)
+    achieved = bytes_alg / launches / (kern_avg_ms / 1e3) / 1e9 if launches else 0.0
+    overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "group-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded Philox harness: drops, churn, commands)",
+        "config": {
+            "workload": f"config{args.config}: {G_local} groups/GPU x {R} replicas"
+                        + (", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step"
+                           if args.config == 3 else ""),
+            "groups_total": total_groups, "replicas": R, "log_cap": log_cap,
+            "steps_per_launch": spl or 1, "parallelism": f"shard-by-group x{world}",
+            "counter_allreduce_every": args.reduce_every if world > 1 else None,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "step_kernel", "kernel_avg_ms": kern_avg_ms, "launches": launches,
+            "alg_bytes_per_launch": bytes_alg / max(1, launches),
+        },
+        "valid": overflow == 0,
+        "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, kw, log_cap)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

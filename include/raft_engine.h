@@ -1,0 +1,243 @@
+/*
+ * raft_engine.h — C-ABI of the MI355X batched Raft engine.
+ *
+ * Drop-in boundary for the consensus core of arodionov/raft-kotlin
+ * (reference: src/main/kotlin/ua/org/kug/raft/RaftServer.kt, Commons.kt,
+ * src/main/proto/greeter.proto).  The reference exposes one Raft node per JVM
+ * process behind the gRPC service
+ *
+ *     service Raft { rpc Vote(RequestVoteRPC) returns (ResponseVoteRPC);
+ *                    rpc Append(RequestAppendEntriesRPC) returns (ResponseAppendEntriesRPC); }
+ *                                                             (greeter.proto:46-49)
+ *
+ * implemented by RaftServer.vote()  (RaftServer.kt:228-251) and
+ *                RaftServer.append() (RaftServer.kt:253-287),
+ * and drives itself from timers: the election timer (Commons.kt:10-31,
+ * RaftServer.kt:180-185), the candidate loop leaderElection()
+ * (RaftServer.kt:187-226) and the leader heartbeat/commit loop
+ * appendRequestAndLeaderHeartbeat() (RaftServer.kt:109-178).
+ *
+ * This engine runs that node state machine for G independent groups of R
+ * replicas each, in deterministic lockstep (one step = one heartbeat period),
+ * with the whole state resident in GPU HBM.  The schedule that turns the
+ * racy reference into a deterministic one is specified in DESIGN.md §3.
+ *
+ * Conventions
+ *   - plain C types only; every function returns RAFT_OK (0) or a negative
+ *     RAFT_E* code; raft_last_error() gives the text (thread-local).
+ *   - the caller owns every host buffer; the engine owns device memory.
+ *   - one engine handle is not reentrant: callers serialise per handle.
+ *   - the reference's per-message exceptions (Log.get IndexOutOfBounds,
+ *     gRPC failures) are per-message status values, never errors.
+ */
+#ifndef RAFT_ENGINE_H
+#define RAFT_ENGINE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAFT_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define RAFT_OK            0
+#define RAFT_EINVAL       -1   /* bad argument                               */
+#define RAFT_ENOMEM       -2   /* device/host allocation failed              */
+#define RAFT_EDEVICE      -3   /* HIP runtime error                          */
+#define RAFT_ERANGE       -4   /* group range outside the engine             */
+#define RAFT_ENODEV       -5   /* no HIP device / kernel image unavailable   */
+
+/* ---- node roles: enum class State (RaftServer.kt:24-26) --------------- */
+#define RAFT_FOLLOWER  0
+#define RAFT_CANDIDATE 1
+#define RAFT_LEADER    2
+
+#define RAFT_MAX_R 8
+
+/* ---- command-injection modes (harness) ---------------- */
+#define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */
+#define RAFT_CMD_ALL_LEADERS   1   /* appendCommand on every LEADER          */
+
+/*
+ * Engine parameters.  The *_ms defaults are the reference's hard-coded
+ * constants; raft_params_default() fills them in.
+ */
+typedef struct raft_params {
+    int32_t  R;                 /* replicas per group, 1..8 (servers.size, RaftServer.kt:307)      */
+    int32_t  log_cap;           /* physical log slots per replica (ghost tail included, §3.2)      */
+    int64_t  G;                 /* groups held by this engine                                      */
+    int64_t  g0;                /* global id of this engine's first group (sharding offset)         */
+    uint64_t seed;              /* Philox key = (seed lo32, seed hi32)                              */
+
+    int32_t  heartbeat_ms;      /* 2000   fixedRateTimer(period = 2000)   RaftServer.kt:115         */
+    int32_t  election_min_ms;   /* 20000  (20_000..23_000).random()       Commons.kt:23             */
+    int32_t  election_max_ms;   /* 23000                                                            */
+    int32_t  backoff_min_ms;    /* 2000   delay((2_000..3_000).random())  RaftServer.kt:221         */
+    int32_t  backoff_max_ms;    /* 3000                                                             */
+    int32_t  round_timeout_ms;  /* 25000  countDownLatch.await(25, SECONDS) RaftServer.kt:189,:214  */
+    int32_t  retry_ms;          /* 5000   retry(delay = 5000)             Commons.kt:37             */
+
+    uint32_t drop_ppm;          /* Bernoulli drop per request and per response (self never dropped) */
+    uint32_t churn_ppm;         /* per group-step probability to isolate the lowest-id LEADER      */
+    int32_t  churn_steps;       /* isolation length in steps                                        */
+    int32_t  partition_period;  /* 0 = off; else a 2-way partition drawn every period steps ...    */
+    int32_t  partition_len;     /* ... holding for partition_len steps                              */
+    uint32_t cmd_ppm;           /* per group-step probability of one client command               */
+    int32_t  cmd_mode;          /* RAFT_CMD_*                                                       */
+    int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
+    int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch (0 = auto)         */
+    int32_t  reserved[7];
+} raft_params;
+
+/* ---- per-step counters (sum over the engine's groups) ------------------ */
+enum raft_counter {
+    RAFT_C_LEADERS = 0,         /* replicas with role LEADER at step end                        */
+    RAFT_C_GROUPS_WITH_LEADER,  /* groups with >= 1 LEADER at step end                          */
+    RAFT_C_TIMEOUTS,            /* election timers fired (Commons.kt:25-27)                     */
+    RAFT_C_ROUNDS,              /* election rounds started (RaftServer.kt:191-193)              */
+    RAFT_C_VOTES_GRANTED,       /* vote() handler grants (RaftServer.kt:237-242)                */
+    RAFT_C_LEADERS_ELECTED,     /* heartbeat sessions started (RaftServer.kt:66,:109)           */
+    RAFT_C_SESSIONS_TICKED,     /* H: leader ticks that built requests (RaftServer.kt:115-122)  */
+    RAFT_C_APPEND_SENT,         /* AppendEntries requests built (incl. self)                    */
+    RAFT_C_APPEND_SKIPPED,      /* Q11: Log.get threw while building (RaftServer.kt:128)        */
+    RAFT_C_ENTRIES_ACKED,       /* successful entry-carrying responses (RaftServer.kt:157-162)  */
+    RAFT_C_COMMITS,             /* commitIndex += 1 by the leader rule (RaftServer.kt:161-162)  */
+    RAFT_C_MSG_DROPPED,         /* requests + responses lost (drop mask, isolation, partition)  */
+    RAFT_C_COMMANDS,            /* client commands appended (RaftServer.kt:100-107)             */
+    RAFT_C_COMMIT_REGRESSIONS,  /* Q4: follower commitIndex decreased (RaftServer.kt:270-272)   */
+    RAFT_C_DUAL_LEADER_GROUPS,  /* groups with 2+ LEADERs in one term at step end (safety flag) */
+    RAFT_C_LOG_OVERFLOW,        /* Log.add refused for lack of physical capacity (run invalid)  */
+    RAFT_C_PREV_READS_LEADER,   /* P_L: log[prev].term reads at the leader                      */
+    RAFT_C_ENTRY_READS_LEADER,  /* E_L: log[i-1] reads at the leader                            */
+    RAFT_C_PREV_READS_FOLLOWER, /* P_F: log[prev].term reads in append()                        */
+    RAFT_C_ENTRY_WRITES,        /* E_W: Log.add stores from append()                            */
+    RAFT_C_VOTE_LOG_READS,      /* V: last-log-term reads in the vote path                      */
+    RAFT_NUM_COUNTERS
+};
+#define RAFT_COUNTER_STRIDE 32  /* int64 slots per step in counter buffers */
+
+/* ---- canonical state export ------------------------------------------- */
+/*
+ * Per-replica scalar fields (int32).  Exported per group as
+ *   [R][RAFT_NUM_FIELDS] scalars, then next[R][R], match[R][R] (leader
+ *   session of replica s towards replica d at [s][d]), then RAFT_GROUP_EXTRA
+ *   harness words; i.e. raft_group_words(R) int32 per group.
+ */
+enum raft_field {
+    RAFT_F_TERM = 0,     /* currentTerm        RaftServer.kt:35-36   */
+    RAFT_F_VOTED,        /* votedFor (-1/id)   RaftServer.kt:38-39   */
+    RAFT_F_ROLE,         /* state              RaftServer.kt:41-42   */
+    RAFT_F_COMMIT,       /* commitIndex        RaftServer.kt:46      */
+    RAFT_F_LAST,         /* log.lastIndex      Commons.kt:49         */
+    RAFT_F_PHYS,         /* physical ArrayList size (ghost tail)     */
+    RAFT_F_ELECTION_MS,  /* election timer remaining (0 if disarmed) */
+    RAFT_F_FLAGS,        /* RAFT_FL_* bits below                      */
+    RAFT_F_PHASE_MS,     /* round elapsed ms, or backoff remaining    */
+    RAFT_F_RETRY_MS,     /* vote retry countdown                      */
+    RAFT_NUM_FIELDS
+};
+#define RAFT_FL_ARMED        (1u << 0)   /* election timer scheduled           */
+#define RAFT_FL_ELECTING     (1u << 1)   /* consumer busy in leaderElection()  */
+#define RAFT_FL_PENDING_RST  (1u << 2)   /* FOLLOWER send queued while busy    */
+#define RAFT_FL_HB_ACTIVE    (1u << 3)   /* heartbeat session running          */
+#define RAFT_FL_BACKOFF      (1u << 4)   /* election loop in backoff delay     */
+#define RAFT_FL_PENDING_SHIFT 8          /* 8 bits: vote dsts awaiting retry   */
+#define RAFT_FL_VOTES_SHIFT   16         /* 4 bits: votesGranted               */
+#define RAFT_FL_LATCH_SHIFT   20         /* 4 bits: responses counted on latch */
+
+#define RAFT_GROUP_EXTRA 2   /* [0] isolation word (rem<<8 | replica), [1] commands issued */
+
+static inline int32_t raft_group_words(int32_t R) {
+    return R * RAFT_NUM_FIELDS + 2 * R * R + RAFT_GROUP_EXTRA;
+}
+
+/* ---- single-handler messages (greeter.proto:16-44, fixed width) -------- */
+typedef struct raft_vote_req {       /* RequestVoteRPC  greeter.proto:16-21 */
+    int32_t term, candidate_id, last_log_index, last_log_term;
+} raft_vote_req;
+typedef struct raft_vote_resp {      /* ResponseVoteRPC greeter.proto:23-26 */
+    int32_t term, vote_granted;
+} raft_vote_resp;
+typedef struct raft_append_req {     /* RequestAppendEntriesRPC greeter.proto:28-39 */
+    int32_t  term, leader_id, prev_log_index, prev_log_term;
+    int32_t  has_entry;              /* entriesCount > 0 (only entries[0] is used, RaftServer.kt:278) */
+    int32_t  entry_term;             /* LogEntry.term                          */
+    uint32_t entry_cmd;              /* LogEntry.command, interned to a u32 id */
+    int32_t  leader_commit;
+} raft_append_req;
+typedef struct raft_append_resp {    /* ResponseAppendEntriesRPC greeter.proto:41-44 */
+    int32_t term, success;
+    int32_t status;                  /* 0 ok; 1 = handler threw (Log index < -1), no response */
+} raft_append_resp;
+
+typedef struct raft_engine raft_engine;
+
+/* ---- lifecycle -------------------------------------------------------- */
+void        raft_params_default(raft_params* p);
+const char* raft_last_error(void);
+int         raft_abi_version(void);
+int raft_engine_create(const raft_params* p, int device, raft_engine** out);
+int raft_engine_destroy(raft_engine* e);
+
+/* ---- the hot path ------------------------------------------------------ */
+/* Advance every group by n_steps lockstep steps.
+ * counters_host: nullable, [n_steps][RAFT_COUNTER_STRIDE] int64, filled in
+ * step order.  Synchronous: returns after the device finished. */
+int raft_engine_step(raft_engine* e, int32_t n_steps, int64_t* counters_host);
+/* Same, asynchronous on the engine stream; counters_dev is a nullable
+ * DEVICE pointer to [n_steps][RAFT_COUNTER_STRIDE] int64 (overwritten). */
+int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_dev);
+int raft_engine_sync(raft_engine* e);
+/* hipStream_t of the engine, as void* (for event timing by the caller). */
+void*   raft_engine_stream(raft_engine* e);
+/* Kernel timing: while enabled, every step-kernel launch is bracketed by a
+ * pair of HIP events on the engine stream.  raft_engine_kernel_time()
+ * synchronises, returns the summed step-kernel milliseconds and launch count
+ * since the last call, and resets them. */
+int raft_engine_set_kernel_timing(raft_engine* e, int enable);
+int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches);
+int64_t raft_engine_step_index(raft_engine* e);   /* steps executed so far */
+int64_t raft_engine_device_bytes(raft_engine* e); /* HBM owned by the engine */
+
+/* ---- state access (fixtures, parity) ----------------------------------- */
+/* out: [n][raft_group_words(R)] int32, canonical layout above. */
+int raft_engine_read_state(raft_engine* e, int64_t g0, int64_t n, int32_t* out);
+int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t* in);
+/* terms/cmds: [n][R][log_cap]; slots >= physLen are unspecified. */
+int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds);
+int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds);
+/* Order-independent 64-bit digest of the full canonical state (logs to
+ * physLen included): sum over groups of a per-group hash. */
+int raft_engine_digest(raft_engine* e, uint64_t* out);
+
+/* ---- single-handler batches: the service boundary ----------------------
+ * group: engine-local group index; dst: replica index 0..R-1.  Messages
+ * to the same (group, dst) are applied in batch order.  Effects on the
+ * consumer (timer reset) use the engine's current step index. */
+int raft_vote_batch(raft_engine* e, const int64_t* group, const int32_t* dst,
+                    const raft_vote_req* req, raft_vote_resp* resp, int64_t n);
+int raft_append_batch(raft_engine* e, const int64_t* group, const int32_t* dst,
+                      const raft_append_req* req, raft_append_resp* resp, int64_t n);
+/* appendCommand (RaftServer.kt:100-107): log.add(lastIndex, (currentTerm, cmd)). */
+int raft_append_command_batch(raft_engine* e, const int64_t* group, const int32_t* replica,
+                              const uint32_t* cmd, int64_t n);
+
+/* ---- Philox4x32-10 (shared bit-for-bit with the CPU harness) -----------
+ * Counter = (c0 = step, c1 = global group id, c2 = purpose, c3 = sub),
+ * key = (seed lo32, seed hi32).  Purposes: */
+#define RAFT_RNG_TIMER        1u  /* sub = replica >> 2, word replica & 3: timeout   */
+#define RAFT_RNG_BACKOFF      2u  /* sub = replica >> 2, word replica & 3: backoff   */
+#define RAFT_RNG_VOTE_DROP    3u  /* sub = src | chunk << 8: 16-bit drop uniforms */
+#define RAFT_RNG_APPEND_DROP  4u  /* sub = src | chunk << 8                        */
+#define RAFT_RNG_HARNESS      5u  /* sub = 0: w0 churn, w1 command, w2 command id  */
+#define RAFT_RNG_PARTITION    6u  /* c0 = partition window start, sub = 0: w0 mask */
+#define RAFT_RNG_INIT_STEP    0xFFFFFFFFu  /* c0 of the initial timer draws        */
+void raft_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAFT_ENGINE_H */

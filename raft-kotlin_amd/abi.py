@@ -1,0 +1,199 @@
+"""ctypes mirror of include/raft_engine.h (the engine's C-ABI).
+
+Pure data definitions: structs, constants, and the loader of the HIP engine
+library.  The loader never falls back to anything: if the in-tree
+``lib/libraft_engine.so`` is missing it raises, so a GPU run cannot silently
+take another path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libraft_engine.so")
+
+RAFT_OK = 0
+RAFT_EINVAL = -1
+RAFT_ENOMEM = -2
+RAFT_EDEVICE = -3
+RAFT_ERANGE = -4
+RAFT_ENODEV = -5
+
+# enum class State (RaftServer.kt:24-26)
+FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
+MAX_R = 8
+
+CMD_LOWEST_LEADER = 0
+CMD_ALL_LEADERS = 1
+
+COUNTER_NAMES = [
+    "leaders", "groups_with_leader", "timeouts", "rounds", "votes_granted",
+    "leaders_elected", "sessions_ticked", "append_sent", "append_skipped",
+    "entries_acked", "commits", "msg_dropped", "commands", "commit_regressions",
+    "dual_leader_groups", "log_overflow", "prev_reads_leader",
+    "entry_reads_leader", "prev_reads_follower", "entry_writes", "vote_log_reads",
+]
+NUM_COUNTERS = len(COUNTER_NAMES)
+COUNTER_STRIDE = 32
+C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
+
+FIELD_NAMES = ["term", "voted", "role", "commit", "last", "phys",
+               "election_ms", "flags", "phase_ms", "retry_ms"]
+NUM_FIELDS = len(FIELD_NAMES)
+F_INDEX = {n: i for i, n in enumerate(FIELD_NAMES)}
+FL_ARMED, FL_ELECTING, FL_PENDING_RST, FL_HB_ACTIVE, FL_BACKOFF = 1, 2, 4, 8, 16
+GROUP_EXTRA = 2
+
+
+def group_words(R: int) -> int:
+    return R * NUM_FIELDS + 2 * R * R + GROUP_EXTRA
+
+
+class raft_params(C.Structure):
+    _fields_ = [
+        ("R", C.c_int32), ("log_cap", C.c_int32), ("G", C.c_int64), ("g0", C.c_int64),
+        ("seed", C.c_uint64),
+        ("heartbeat_ms", C.c_int32), ("election_min_ms", C.c_int32), ("election_max_ms", C.c_int32),
+        ("backoff_min_ms", C.c_int32), ("backoff_max_ms", C.c_int32),
+        ("round_timeout_ms", C.c_int32), ("retry_ms", C.c_int32),
+        ("drop_ppm", C.c_uint32), ("churn_ppm", C.c_uint32), ("churn_steps", C.c_int32),
+        ("partition_period", C.c_int32), ("partition_len", C.c_int32),
+        ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
+        ("steps_per_launch", C.c_int32), ("reserved", C.c_int32 * 7),
+    ]
+
+
+class raft_vote_req(C.Structure):
+    _fields_ = [("term", C.c_int32), ("candidate_id", C.c_int32),
+                ("last_log_index", C.c_int32), ("last_log_term", C.c_int32)]
+
+
+class raft_vote_resp(C.Structure):
+    _fields_ = [("term", C.c_int32), ("vote_granted", C.c_int32)]
+
+
+class raft_append_req(C.Structure):
+    _fields_ = [("term", C.c_int32), ("leader_id", C.c_int32), ("prev_log_index", C.c_int32),
+                ("prev_log_term", C.c_int32), ("has_entry", C.c_int32), ("entry_term", C.c_int32),
+                ("entry_cmd", C.c_uint32), ("leader_commit", C.c_int32)]
+
+
+class raft_append_resp(C.Structure):
+    _fields_ = [("term", C.c_int32), ("success", C.c_int32), ("status", C.c_int32)]
+
+
+# the reference's hard-coded constants
+DEFAULTS = dict(
+    heartbeat_ms=2000,        # RaftServer.kt:115
+    election_min_ms=20000,    # Commons.kt:23
+    election_max_ms=23000,
+    backoff_min_ms=2000,      # RaftServer.kt:221
+    backoff_max_ms=3000,
+    round_timeout_ms=25000,   # RaftServer.kt:189, :214
+    retry_ms=5000,            # Commons.kt:37
+)
+
+# BASELINE.json configs; G/steps are the full sizes
+CONFIGS = {
+    1: dict(R=5, G=1, seed=1, cmd_ppm=1_000_000, cmd_mode=CMD_LOWEST_LEADER, cmd_limit=1000),
+    2: dict(R=3, G=10_000, seed=2, cmd_ppm=250_000, cmd_mode=CMD_LOWEST_LEADER),
+    3: dict(R=5, G=1_000_000, seed=3, drop_ppm=50_000, churn_ppm=1_000, churn_steps=15,
+            cmd_ppm=250_000, cmd_mode=CMD_LOWEST_LEADER),
+    5: dict(R=7, G=100_000, seed=5, partition_period=50, partition_len=25,
+            cmd_ppm=1_000_000, cmd_mode=CMD_ALL_LEADERS),
+}
+CONFIG_STEPS = {1: None, 2: 1_000, 3: 10_000, 5: 10_000}
+
+
+def make_params(**kw) -> raft_params:
+    """raft_params with the reference defaults; keyword overrides."""
+    p = raft_params()
+    p.R = 5
+    p.log_cap = 1024
+    p.G = 1
+    p.g0 = 0
+    p.seed = 1
+    for k, v in DEFAULTS.items():
+        setattr(p, k, v)
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown raft_params field {k!r}")
+        setattr(p, k, v)
+    return p
+
+
+def config_params(cfg: int, **kw) -> raft_params:
+    d = dict(CONFIGS[cfg])
+    d.update(kw)
+    return make_params(**d)
+
+
+def counters_array(n_steps: int) -> np.ndarray:
+    return np.zeros((n_steps, COUNTER_STRIDE), dtype=np.int64)
+
+
+def ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+_lib = None
+
+
+def load_library(path: str | None = None):
+    """Load the HIP engine.  Raises if it is absent: there is no fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"HIP engine library not built: {p} (run `python __graft_entry__.py build` "
+            "or `python raft-kotlin_amd/build.py`)")
+    lib = C.CDLL(p)
+    P, I32, I64, U64 = C.POINTER, C.c_int32, C.c_int64, C.c_uint64
+    eng = C.c_void_p
+    sig = {
+        "raft_params_default": (None, [P(raft_params)]),
+        "raft_last_error": (C.c_char_p, []),
+        "raft_abi_version": (C.c_int, []),
+        "raft_engine_create": (C.c_int, [P(raft_params), C.c_int, P(eng)]),
+        "raft_engine_destroy": (C.c_int, [eng]),
+        "raft_engine_step": (C.c_int, [eng, I32, P(I64)]),
+        "raft_engine_step_async": (C.c_int, [eng, I32, C.c_void_p]),
+        "raft_engine_sync": (C.c_int, [eng]),
+        "raft_engine_stream": (C.c_void_p, [eng]),
+        "raft_engine_set_kernel_timing": (C.c_int, [eng, C.c_int]),
+        "raft_engine_kernel_time": (C.c_int, [eng, P(C.c_double), P(I64)]),
+        "raft_engine_step_index": (I64, [eng]),
+        "raft_engine_device_bytes": (I64, [eng]),
+        "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
+        "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
+        "raft_engine_read_log": (C.c_int, [eng, I64, I64, P(I32), P(C.c_uint32)]),
+        "raft_engine_write_log": (C.c_int, [eng, I64, I64, P(I32), P(C.c_uint32)]),
+        "raft_engine_digest": (C.c_int, [eng, P(U64)]),
+        "raft_vote_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_vote_req), P(raft_vote_resp), I64]),
+        "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
+        "raft_append_command_batch": (C.c_int, [eng, P(I64), P(I32), P(C.c_uint32), I64]),
+        "raft_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib if path is None else _lib
+    return lib
+
+
+# symbols declared in include/raft_engine.h (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = [
+    "raft_params_default", "raft_last_error", "raft_abi_version", "raft_engine_create",
+    "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
+    "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
+    "raft_engine_step_index", "raft_engine_device_bytes",
+    "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
+    "raft_engine_write_log", "raft_engine_digest", "raft_vote_batch", "raft_append_batch",
+    "raft_append_command_batch", "raft_philox4x32_10",
+]

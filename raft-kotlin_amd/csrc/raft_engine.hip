@@ -1,0 +1,791 @@
+// raft_engine.hip — HIP kernels (gfx950) and the C-ABI of include/raft_engine.h.
+//
+// HBM layout (structure of arrays, lane = group, so every state access of a
+// wave is one contiguous 256-byte run per field):
+//   st  int32 [RAFT_NUM_FIELDS][R][G]     per-replica scalars (RaftServer.kt:35-48)
+//   nx  int32 [R][R][G]                   nextIndex  of replica s's session towards d
+//   mt  int32 [R][R][G]                   matchIndex (RaftServer.kt:112-113)
+//   gx  int32 [2][G]                      harness words (isolation, commands issued)
+//   log uint2 [G][R][log_cap]             (term, cmd) physical log slots (Commons.kt:51)
+// The step kernel keeps a group in VGPRs for the whole launch (1..K fused
+// lockstep steps) and touches HBM only for the state load/store at the launch
+// edges and the log slots the handlers read or write.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "raft_step.h"
+
+using namespace raft;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return fail(RAFT_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct DevState {
+    int32_t* st;
+    int32_t* nx;
+    int32_t* mt;
+    int32_t* gx;
+    uint2* log;
+};
+
+constexpr int BLOCK = 256;
+constexpr int WAVES_PER_BLOCK = BLOCK / 64;
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// state <-> registers
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64_t G, int64_t i, uint32_t& sess) {
+#define LD(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        g.term[r] = LD(RAFT_F_TERM, r);
+        g.voted[r] = LD(RAFT_F_VOTED, r);
+        g.role[r] = LD(RAFT_F_ROLE, r);
+        g.commit[r] = LD(RAFT_F_COMMIT, r);
+        g.last[r] = LD(RAFT_F_LAST, r);
+        g.phys[r] = LD(RAFT_F_PHYS, r);
+        g.elec[r] = LD(RAFT_F_ELECTION_MS, r);
+        g.fl[r] = (uint32_t)LD(RAFT_F_FLAGS, r);
+        g.phase[r] = LD(RAFT_F_PHASE_MS, r);
+        g.retry[r] = LD(RAFT_F_RETRY_MS, r);
+    }
+#undef LD
+    sess = 0;
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+        if (g.fl[s] & FL_HB) {
+            sess |= 1u << s;
+#pragma unroll
+            for (int d = 0; d < R; ++d) {
+                g.nx[s][d] = S.nx[((int64_t)s * R + d) * G + i];
+                g.mc[s][d] = S.mt[((int64_t)s * R + d) * G + i];
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < R; ++d) { g.nx[s][d] = 0; g.mc[s][d] = 0; }
+        }
+    }
+    g.iso = S.gx[i];
+    g.cmdc = S.gx[G + i];
+}
+
+template <int R>
+__device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S, int64_t G, int64_t i, uint32_t sess) {
+#define ST(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        ST(RAFT_F_TERM, r) = g.term[r];
+        ST(RAFT_F_VOTED, r) = g.voted[r];
+        ST(RAFT_F_ROLE, r) = g.role[r];
+        ST(RAFT_F_COMMIT, r) = g.commit[r];
+        ST(RAFT_F_LAST, r) = g.last[r];
+        ST(RAFT_F_PHYS, r) = g.phys[r];
+        ST(RAFT_F_ELECTION_MS, r) = g.elec[r];
+        ST(RAFT_F_FLAGS, r) = (int32_t)(g.fl[r] & FL_EXPORT_MASK);
+        ST(RAFT_F_PHASE_MS, r) = g.phase[r];
+        ST(RAFT_F_RETRY_MS, r) = g.retry[r];
+    }
+#undef ST
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+        if ((sess >> s) & 1u) {
+#pragma unroll
+            for (int d = 0; d < R; ++d) {
+                S.nx[((int64_t)s * R + d) * G + i] = g.nx[s][d];
+                S.mt[((int64_t)s * R + d) * G + i] = g.mc[s][d];
+            }
+        }
+    }
+    S.gx[i] = g.iso;
+    S.gx[G + i] = g.cmdc;
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(BLOCK) void init_kernel(DevState S, DevParams p) {
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= p.G) return;
+    const int64_t G = p.G;
+    const uint32_t gid = (uint32_t)(p.g0 + i);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) S.st[((int64_t)f * R + r) * G + i] = 0;
+        S.st[((int64_t)RAFT_F_VOTED * R + r) * G + i] = -1;                 // RaftServer.kt:39
+        // the timer started by init (RaftServer.kt:58, Commons.kt:14)
+        const u32x4 w = draw(p, RAFT_RNG_INIT_STEP, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
+        S.st[((int64_t)RAFT_F_ELECTION_MS * R + r) * G + i] = scale_range(word_of(w, r & 3), p.emin, p.emax);
+        S.st[((int64_t)RAFT_F_FLAGS * R + r) * G + i] = (int32_t)FL_ARMED;
+#pragma unroll
+        for (int d = 0; d < R; ++d) {
+            S.nx[((int64_t)r * R + d) * G + i] = 0;
+            S.mt[((int64_t)r * R + d) * G + i] = 0;
+        }
+    }
+    S.gx[i] = 0;
+    S.gx[G + i] = 0;
+}
+
+// K lockstep steps of every group; per-step per-block counter partials.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, uint32_t t0, int nsteps,
+                                                     int32_t* __restrict__ partials) {
+    __shared__ int red[WAVES_PER_BLOCK][NC];
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const bool live = i < p.G;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    Group<R> g;
+    uint32_t sess = 0;
+    if (live) load_group<R>(g, S, p.G, i, sess);
+    else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            g.term[r] = g.voted[r] = g.role[r] = g.commit[r] = g.last[r] = g.phys[r] = 0;
+            g.elec[r] = g.phase[r] = g.retry[r] = 0;
+            g.fl[r] = 0;
+#pragma unroll
+            for (int d = 0; d < R; ++d) g.nx[r][d] = g.mc[r][d] = 0;
+        }
+        g.iso = g.cmdc = 0;
+    }
+    Stepper<R> st;
+    for (int k = 0; k < nsteps; ++k) {
+        int cnt[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) cnt[c] = 0;
+        Ctx ctx{t0 + (uint32_t)k, (uint32_t)(p.g0 + i), -1, 0u,
+                p.log + (live ? i : 0) * (int64_t)R * p.cap, p.cap, cnt};
+        if (live) {
+            st.step(g, p, ctx);
+#pragma unroll
+            for (int s = 0; s < R; ++s) sess |= (g.fl[s] & FL_HB) ? (1u << s) : 0u;
+        }
+        // block partial of every counter for this step (no atomics: written, then reduced)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int v = wave_sum(cnt[c]);
+            if (lane == 0) red[wave][c] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < NC) {
+            int v = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES_PER_BLOCK; ++w) v += red[w][threadIdx.x];
+            partials[((int64_t)k * gridDim.x + blockIdx.x) * NC + threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    if (live) store_group<R>(g, S, p.G, i, sess);
+}
+
+// counters[k][c] = sum over blocks of partials[k][b][c]   (grid = steps)
+__global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const int32_t* __restrict__ partials, int nblocks,
+                                                                int64_t* __restrict__ counters) {
+    __shared__ int64_t acc[BLOCK];
+    const int k = blockIdx.x;
+    const int c = threadIdx.x % 32, part = threadIdx.x / 32;   // 8 partial sums per counter
+    int64_t v = 0;
+    if (c < NC)
+        for (int b = part; b < nblocks; b += BLOCK / 32) v += partials[((int64_t)k * nblocks + b) * NC + c];
+    acc[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x < RAFT_COUNTER_STRIDE) {
+        int64_t s = 0;
+        for (int q = 0; q < BLOCK / 32; ++q) s += acc[q * 32 + threadIdx.x];
+        counters[(int64_t)k * RAFT_COUNTER_STRIDE + threadIdx.x] = threadIdx.x < NC ? s : 0;
+    }
+}
+
+// canonical export [n][W] of groups [g0, g0+n)
+template <int R>
+__global__ __launch_bounds__(BLOCK) void pack_kernel(DevState S, int64_t G, int64_t g0, int64_t n, int32_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const int64_t i = g0 + j;
+    constexpr int W = R * RAFT_NUM_FIELDS + 2 * R * R + RAFT_GROUP_EXTRA;
+    int32_t* w = out + j * W;
+    for (int r = 0; r < R; ++r)
+        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) w[r * RAFT_NUM_FIELDS + f] = S.st[((int64_t)f * R + r) * G + i];
+    for (int s = 0; s < R; ++s)
+        for (int d = 0; d < R; ++d) {
+            w[R * RAFT_NUM_FIELDS + s * R + d] = S.nx[((int64_t)s * R + d) * G + i];
+            w[R * RAFT_NUM_FIELDS + R * R + s * R + d] = S.mt[((int64_t)s * R + d) * G + i];
+        }
+    w[W - 2] = S.gx[i];
+    w[W - 1] = S.gx[G + i];
+}
+
+template <int R>
+__global__ __launch_bounds__(BLOCK) void unpack_kernel(DevState S, int64_t G, int64_t g0, int64_t n, const int32_t* in) {
+    const int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const int64_t i = g0 + j;
+    constexpr int W = R * RAFT_NUM_FIELDS + 2 * R * R + RAFT_GROUP_EXTRA;
+    const int32_t* w = in + j * W;
+    for (int r = 0; r < R; ++r)
+        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) S.st[((int64_t)f * R + r) * G + i] = w[r * RAFT_NUM_FIELDS + f];
+    for (int s = 0; s < R; ++s)
+        for (int d = 0; d < R; ++d) {
+            S.nx[((int64_t)s * R + d) * G + i] = w[R * RAFT_NUM_FIELDS + s * R + d];
+            S.mt[((int64_t)s * R + d) * G + i] = w[R * RAFT_NUM_FIELDS + R * R + s * R + d];
+        }
+    S.gx[i] = w[W - 2];
+    S.gx[G + i] = w[W - 1];
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// order-independent state digest: sum of per-group FNV-1a/fmix64
+template <int R>
+__global__ __launch_bounds__(BLOCK) void digest_kernel(DevState S, DevParams p, unsigned long long* out) {
+    __shared__ unsigned long long part[WAVES_PER_BLOCK];
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const int64_t G = p.G;
+    uint64_t hv = 0;
+    if (i < G) {
+        uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)(p.g0 + i) * 0x9E3779B97F4A7C15ull);
+        auto feed = [&](int32_t v) { h ^= (uint32_t)v; h *= 0x100000001b3ull; };
+        for (int r = 0; r < R; ++r) {
+            for (int f = 0; f < RAFT_NUM_FIELDS; ++f) feed(S.st[((int64_t)f * R + r) * G + i]);
+            for (int d = 0; d < R; ++d) feed(S.nx[((int64_t)r * R + d) * G + i]);
+            for (int d = 0; d < R; ++d) feed(S.mt[((int64_t)r * R + d) * G + i]);
+            const int32_t phys = S.st[((int64_t)RAFT_F_PHYS * R + r) * G + i];
+            const uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
+            for (int32_t j = 0; j < phys; ++j) { const uint2 e = lr[j]; feed((int32_t)e.x); feed((int32_t)e.y); }
+        }
+        feed(S.gx[i]);
+        feed(S.gx[G + i]);
+        hv = fmix64(h);
+    }
+    // wave sum of 64-bit values
+    uint32_t lo = (uint32_t)hv, hi = (uint32_t)(hv >> 32);
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t olo = __shfl_xor(lo, o, 64), ohi = __shfl_xor(hi, o, 64);
+        const uint64_t s = ((uint64_t)hi << 32 | lo) + ((uint64_t)ohi << 32 | olo);
+        lo = (uint32_t)s; hi = (uint32_t)(s >> 32);
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = (uint64_t)hi << 32 | lo;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int w = 0; w < WAVES_PER_BLOCK; ++w) s += part[w];
+        atomicAdd(out, s);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// single-handler batches: one lane per distinct (group, replica), its
+// messages applied in batch order
+// ---------------------------------------------------------------------------
+struct RepState {
+    int32_t term, voted, role, commit, last, phys, elec, phase, retry;
+    uint32_t fl;
+    __device__ Rep ref() { return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl}; }
+};
+
+__device__ __forceinline__ void load_rep(RepState& x, const DevState& S, int R, int64_t G, int64_t i, int r) {
+#define LD(f) S.st[((int64_t)(f) * R + r) * G + i]
+    x.term = LD(RAFT_F_TERM); x.voted = LD(RAFT_F_VOTED); x.role = LD(RAFT_F_ROLE); x.commit = LD(RAFT_F_COMMIT);
+    x.last = LD(RAFT_F_LAST); x.phys = LD(RAFT_F_PHYS); x.elec = LD(RAFT_F_ELECTION_MS);
+    x.fl = (uint32_t)LD(RAFT_F_FLAGS); x.phase = LD(RAFT_F_PHASE_MS); x.retry = LD(RAFT_F_RETRY_MS);
+#undef LD
+}
+
+__device__ __forceinline__ void store_rep(const RepState& x, const DevState& S, int R, int64_t G, int64_t i, int r) {
+#define ST(f) S.st[((int64_t)(f) * R + r) * G + i]
+    ST(RAFT_F_TERM) = x.term; ST(RAFT_F_VOTED) = x.voted; ST(RAFT_F_ROLE) = x.role; ST(RAFT_F_COMMIT) = x.commit;
+    ST(RAFT_F_LAST) = x.last; ST(RAFT_F_PHYS) = x.phys; ST(RAFT_F_ELECTION_MS) = x.elec;
+    ST(RAFT_F_FLAGS) = (int32_t)(x.fl & FL_EXPORT_MASK); ST(RAFT_F_PHASE_MS) = x.phase; ST(RAFT_F_RETRY_MS) = x.retry;
+#undef ST
+}
+
+__device__ __forceinline__ void resolve_rep_draw(RepState& x, const DevParams& p, uint32_t t, uint32_t gid, int r) {
+    if (x.fl & FL_DRAW) {
+        const u32x4 w = draw(p, t, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
+        x.elec = scale_range(word_of(w, r & 3), p.emin, p.emax);
+        x.fl &= ~FL_DRAW;
+    }
+}
+
+enum { BATCH_VOTE = 0, BATCH_APPEND = 1, BATCH_COMMAND = 2 };
+
+// keys[k] = group * R + replica; msgs of key k are order[off[k] .. off[k+1])
+__global__ __launch_bounds__(BLOCK) void batch_kernel(DevState S, DevParams p, uint32_t t, int kind, int nkeys,
+                                                      const int64_t* keys, const int64_t* off, const int64_t* order,
+                                                      const void* req, void* resp) {
+    const int k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= nkeys) return;
+    const int R = p.R;
+    const int64_t i = keys[k] / R;
+    const int r = (int)(keys[k] % R);
+    const uint32_t gid = (uint32_t)(p.g0 + i);
+    RepState x;
+    load_rep(x, S, R, p.G, i, r);
+    uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
+    int cnt[NC];
+    for (int m = off[k]; m < off[k + 1]; ++m) {
+        const int64_t o = order[m];
+        if (kind == BATCH_VOTE) {
+            const raft_vote_req q = ((const raft_vote_req*)req)[o];
+            int32_t rt; bool gr;
+            vote_handler(x.ref(), lr, q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
+            ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, gr ? 1 : 0};
+        } else if (kind == BATCH_APPEND) {
+            const raft_append_req q = ((const raft_append_req*)req)[o];
+            int32_t rt = 0; bool su = false;
+            const bool okh = append_handler(x.ref(), r + 1, lr, p.cap, q.term, q.leader_id, q.prev_log_index,
+                                            q.prev_log_term, q.has_entry != 0, Entry{q.entry_term, q.entry_cmd},
+                                            q.leader_commit, cnt, rt, su);
+            ((raft_append_resp*)resp)[o] = raft_append_resp{rt, su ? 1 : 0, okh ? 0 : 1};
+        } else {
+            append_command(x.ref(), lr, p.cap, ((const uint32_t*)req)[o], cnt);
+        }
+        resolve_rep_draw(x, p, t, gid, r);
+    }
+    store_rep(x, S, R, p.G, i, r);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct raft_engine {
+    raft_params p;
+    DevParams dp;
+    int device;
+    hipStream_t stream;
+    DevState S;
+    void* base;
+    size_t bytes;
+    uint64_t t;
+    int K;                      // steps per launch
+    int nblocks;
+    int32_t* partials;          // [K][nblocks][NC]
+    int64_t* counters_dev;      // [K][STRIDE] scratch
+    // step-kernel event timing
+    bool timing;
+    std::vector<hipEvent_t> ev;  // pool, pairs
+    size_t ev_used;
+    int64_t timed_launches;
+};
+
+template <template <int> class Fn, typename... A>
+static void dispatch_R(int R, A&&... a) {
+    switch (R) {
+        case 1: Fn<1>::run(a...); break;
+        case 2: Fn<2>::run(a...); break;
+        case 3: Fn<3>::run(a...); break;
+        case 4: Fn<4>::run(a...); break;
+        case 5: Fn<5>::run(a...); break;
+        case 6: Fn<6>::run(a...); break;
+        case 7: Fn<7>::run(a...); break;
+        case 8: Fn<8>::run(a...); break;
+        default: break;
+    }
+}
+
+template <int R> struct InitL {
+    static void run(raft_engine* e) {
+        const unsigned nb = (unsigned)((e->p.G + BLOCK - 1) / BLOCK);
+        init_kernel<R><<<nb, BLOCK, 0, e->stream>>>(e->S, e->dp);
+    }
+};
+template <int R> struct StepL {
+    static void run(raft_engine* e, uint32_t t0, int k) {
+        step_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->S, e->dp, t0, k, e->partials);
+    }
+};
+template <int R> struct PackL {
+    static void run(raft_engine* e, int64_t g0, int64_t n, int32_t* buf) {
+        pack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->S, e->p.G, g0, n, buf);
+    }
+};
+template <int R> struct UnpackL {
+    static void run(raft_engine* e, int64_t g0, int64_t n, const int32_t* buf) {
+        unpack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->S, e->p.G, g0, n, buf);
+    }
+};
+template <int R> struct DigestL {
+    static void run(raft_engine* e, unsigned long long* out) {
+        digest_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->S, e->dp, out);
+    }
+};
+
+static uint64_t ppm_thr(uint32_t ppm, int bits) {
+    // smallest u with u * 1e6 >= ppm << bits  ==  ceil(ppm * 2^bits / 1e6)
+    const unsigned __int128 num = (unsigned __int128)ppm << bits;
+    return (uint64_t)((num + 999999u) / 1000000u);
+}
+
+extern "C" {
+
+void raft_params_default(raft_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->R = 5;
+    p->log_cap = 1024;
+    p->G = 1;
+    p->g0 = 0;
+    p->seed = 1;
+    p->heartbeat_ms = 2000;
+    p->election_min_ms = 20000;
+    p->election_max_ms = 23000;
+    p->backoff_min_ms = 2000;
+    p->backoff_max_ms = 3000;
+    p->round_timeout_ms = 25000;
+    p->retry_ms = 5000;
+    p->cmd_mode = RAFT_CMD_LOWEST_LEADER;
+}
+
+const char* raft_last_error(void) { return g_err.c_str(); }
+int raft_abi_version(void) { return RAFT_ABI_VERSION; }
+
+void raft_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    const u32x4 v = philox4x32_10(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
+    out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+}
+
+int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
+    if (!p || !out) return fail(RAFT_EINVAL, "null argument");
+    *out = nullptr;
+    if (p->R < 1 || p->R > RAFT_MAX_R) return fail(RAFT_EINVAL, "R must be in 1..8");
+    if (p->G < 1 || p->G > (int64_t)0x7FFFFFFF) return fail(RAFT_EINVAL, "G out of range");
+    if (p->g0 < 0 || p->g0 + p->G > (int64_t)0x100000000ll) return fail(RAFT_EINVAL, "g0 + G exceeds 2^32");
+    if (p->log_cap < 1) return fail(RAFT_EINVAL, "log_cap must be >= 1");
+    if (p->heartbeat_ms <= 0 || p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms)
+        return fail(RAFT_EINVAL, "bad timer constants");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RAFT_ENODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(RAFT_EINVAL, "bad device index");
+    HIP_TRY(hipSetDevice(device));
+
+    raft_engine* e = new raft_engine();
+    e->p = *p;
+    e->timing = false;
+    e->ev_used = 0;
+    e->timed_launches = 0;
+    e->device = device;
+    e->t = 0;
+    const int64_t G = p->G, R = p->R;
+    DevParams& d = e->dp;
+    d.G = G; d.g0 = p->g0; d.R = p->R; d.cap = p->log_cap;
+    d.key0 = (uint32_t)p->seed; d.key1 = (uint32_t)(p->seed >> 32);
+    d.P = p->heartbeat_ms; d.emin = p->election_min_ms; d.emax = p->election_max_ms;
+    d.bmin = p->backoff_min_ms; d.bmax = p->backoff_max_ms; d.round_to = p->round_timeout_ms; d.retry = p->retry_ms;
+    d.drop_ppm = p->drop_ppm; d.drop_thr16 = (uint32_t)ppm_thr(p->drop_ppm, 16);
+    d.churn_thr32 = ppm_thr(p->churn_ppm, 32); d.cmd_thr32 = ppm_thr(p->cmd_ppm, 32);
+    d.churn_steps = p->churn_steps; d.part_period = p->partition_period; d.part_len = p->partition_len;
+    d.cmd_mode = p->cmd_mode; d.cmd_limit = p->cmd_limit;
+    e->nblocks = (int)((G + BLOCK - 1) / BLOCK);
+    e->K = p->steps_per_launch > 0 ? p->steps_per_launch : 1;
+
+    const size_t st_b = (size_t)RAFT_NUM_FIELDS * R * G * 4;
+    const size_t ses_b = (size_t)R * R * G * 4;
+    const size_t gx_b = (size_t)2 * G * 4;
+    const size_t log_b = (size_t)G * R * p->log_cap * 8;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t part_b = (size_t)e->K * e->nblocks * NC * 4;
+    const size_t cnt_b = (size_t)e->K * RAFT_COUNTER_STRIDE * 8;
+    e->bytes = al(st_b) + 2 * al(ses_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
+    hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (err != hipSuccess) { delete e; return fail(RAFT_EDEVICE, "hipStreamCreate failed"); }
+    err = hipMalloc(&e->base, e->bytes);
+    if (err != hipSuccess) {
+        (void)hipStreamDestroy(e->stream);
+        delete e;
+        return fail(RAFT_ENOMEM, "hipMalloc of " + std::to_string(e->bytes) + " bytes failed");
+    }
+    char* b = (char*)e->base;
+    e->S.st = (int32_t*)b; b += al(st_b);
+    e->S.nx = (int32_t*)b; b += al(ses_b);
+    e->S.mt = (int32_t*)b; b += al(ses_b);
+    e->S.gx = (int32_t*)b; b += al(gx_b);
+    e->partials = (int32_t*)b; b += al(part_b);
+    e->counters_dev = (int64_t*)b; b += al(cnt_b);
+    e->S.log = (uint2*)b;
+    d.log = e->S.log;
+    *out = e;
+    dispatch_R<InitL>(p->R, e);
+    err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) {
+        (void)hipFree(e->base);
+        (void)hipStreamDestroy(e->stream);
+        delete e;
+        *out = nullptr;
+        return fail(RAFT_EDEVICE, std::string("init kernel: ") + hipGetErrorString(err));
+    }
+    return RAFT_OK;
+}
+
+int raft_engine_destroy(raft_engine* e) {
+    if (!e) return RAFT_OK;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
+    (void)hipFree(e->base);
+    (void)hipStreamDestroy(e->stream);
+    delete e;
+    return RAFT_OK;
+}
+
+int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_dev) {
+    if (!e || n_steps < 0) return fail(RAFT_EINVAL, "bad argument");
+    HIP_TRY(hipSetDevice(e->device));
+    for (int32_t done = 0; done < n_steps;) {
+        const int k = std::min<int32_t>(e->K, n_steps - done);
+        if (e->timing) {
+            if (e->ev_used + 2 > e->ev.size()) {
+                for (int q = 0; q < 64; ++q) {
+                    hipEvent_t x;
+                    HIP_TRY(hipEventCreate(&x));
+                    e->ev.push_back(x);
+                }
+            }
+            HIP_TRY(hipEventRecord(e->ev[e->ev_used], e->stream));
+        }
+        dispatch_R<StepL>(e->p.R, e, (uint32_t)(e->t + done), k);
+        if (e->timing) {
+            HIP_TRY(hipEventRecord(e->ev[e->ev_used + 1], e->stream));
+            e->ev_used += 2;
+        }
+        int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
+        reduce_counters_kernel<<<k, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, dst);
+        done += k;
+    }
+    HIP_TRY(hipGetLastError());
+    e->t += (uint64_t)n_steps;
+    return RAFT_OK;
+}
+
+int raft_engine_sync(raft_engine* e) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return RAFT_OK;
+}
+
+int raft_engine_step(raft_engine* e, int32_t n_steps, int64_t* counters_host) {
+    if (!e || n_steps < 0) return fail(RAFT_EINVAL, "bad argument");
+    HIP_TRY(hipSetDevice(e->device));
+    for (int32_t done = 0; done < n_steps;) {
+        const int k = std::min<int32_t>(e->K, n_steps - done);
+        const int rc = raft_engine_step_async(e, k, e->counters_dev);
+        if (rc) return rc;
+        if (counters_host)
+            HIP_TRY(hipMemcpyAsync(counters_host + (int64_t)done * RAFT_COUNTER_STRIDE, e->counters_dev,
+                                   (size_t)k * RAFT_COUNTER_STRIDE * 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        done += k;
+    }
+    return RAFT_OK;
+}
+
+void* raft_engine_stream(raft_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int raft_engine_set_kernel_timing(raft_engine* e, int enable) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    e->timing = enable != 0;
+    return RAFT_OK;
+}
+
+int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches) {
+    if (!e || !total_ms || !launches) return fail(RAFT_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    double acc = 0.0;
+    for (size_t q = 0; q + 1 < e->ev_used; q += 2) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e->ev[q], e->ev[q + 1]));
+        acc += ms;
+    }
+    *total_ms = acc;
+    *launches = (int64_t)(e->ev_used / 2);
+    e->ev_used = 0;
+    return RAFT_OK;
+}
+int64_t raft_engine_step_index(raft_engine* e) { return e ? (int64_t)e->t : -1; }
+int64_t raft_engine_device_bytes(raft_engine* e) { return e ? (int64_t)e->bytes : -1; }
+
+static int check_range(raft_engine* e, int64_t g0, int64_t n) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (g0 < 0 || n < 0 || g0 + n > e->p.G) return fail(RAFT_ERANGE, "group range outside the engine");
+    return RAFT_OK;
+}
+
+int raft_engine_read_state(raft_engine* e, int64_t g0, int64_t n, int32_t* out) {
+    if (int rc = check_range(e, g0, n)) return rc;
+    if (n == 0) return RAFT_OK;
+    if (!out) return fail(RAFT_EINVAL, "null buffer");
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t bytes = (size_t)n * raft_group_words(e->p.R) * 4;
+    int32_t* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, bytes));
+    dispatch_R<PackL>(e->p.R, e, g0, n, buf);
+    hipError_t err = hipMemcpyAsync(out, buf, bytes, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
+int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t* in) {
+    if (int rc = check_range(e, g0, n)) return rc;
+    if (n == 0) return RAFT_OK;
+    if (!in) return fail(RAFT_EINVAL, "null buffer");
+    const int W = raft_group_words(e->p.R);
+    for (int64_t j = 0; j < n; ++j)              // invariant 0 <= lastIndex <= physLen <= log_cap
+        for (int r = 0; r < e->p.R; ++r) {
+            const int32_t* f = in + j * W + r * RAFT_NUM_FIELDS;
+            if (f[RAFT_F_LAST] < 0 || f[RAFT_F_LAST] > f[RAFT_F_PHYS] || f[RAFT_F_PHYS] > e->p.log_cap)
+                return fail(RAFT_EINVAL, "state violates 0 <= lastIndex <= physLen <= log_cap");
+        }
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t bytes = (size_t)n * W * 4;
+    int32_t* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, bytes));
+    hipError_t err = hipMemcpyAsync(buf, in, bytes, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess) {
+        dispatch_R<UnpackL>(e->p.R, e, g0, n, buf);
+        err = hipStreamSynchronize(e->stream);
+    }
+    (void)hipFree(buf);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
+int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds) {
+    if (int rc = check_range(e, g0, n)) return rc;
+    if (n == 0) return RAFT_OK;
+    if (!terms || !cmds) return fail(RAFT_EINVAL, "null buffer");
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
+    std::vector<uint2> tmp(cnt);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), e->S.log + (size_t)g0 * e->p.R * e->p.log_cap, cnt * 8,
+                           hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (size_t k = 0; k < cnt; ++k) { terms[k] = (int32_t)tmp[k].x; cmds[k] = tmp[k].y; }
+    return RAFT_OK;
+}
+
+int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds) {
+    if (int rc = check_range(e, g0, n)) return rc;
+    if (n == 0) return RAFT_OK;
+    if (!terms || !cmds) return fail(RAFT_EINVAL, "null buffer");
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
+    std::vector<uint2> tmp(cnt);
+    for (size_t k = 0; k < cnt; ++k) tmp[k] = make_uint2((uint32_t)terms[k], cmds[k]);
+    HIP_TRY(hipMemcpyAsync(e->S.log + (size_t)g0 * e->p.R * e->p.log_cap, tmp.data(), cnt * 8,
+                           hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return RAFT_OK;
+}
+
+int raft_engine_digest(raft_engine* e, uint64_t* out) {
+    if (!e || !out) return fail(RAFT_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(e->device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 8));
+    hipError_t err = hipMemsetAsync(d, 0, 8, e->stream);
+    if (err == hipSuccess) {
+        dispatch_R<DigestL>(e->p.R, e, d);
+        err = hipMemcpyAsync(out, d, 8, hipMemcpyDeviceToHost, e->stream);
+    }
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
+static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                     size_t req_sz, void* resp, size_t resp_sz, int64_t n) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (n < 0) return fail(RAFT_EINVAL, "negative batch");
+    if (n == 0) return RAFT_OK;
+    if (!group || !dst || !req || (resp_sz && !resp)) return fail(RAFT_EINVAL, "null buffer");
+    const int R = e->p.R;
+    std::vector<int64_t> key(n);
+    for (int64_t m = 0; m < n; ++m) {
+        if (group[m] < 0 || group[m] >= e->p.G) return fail(RAFT_ERANGE, "group outside the engine");
+        if (dst[m] < 0 || dst[m] >= R) return fail(RAFT_EINVAL, "replica index outside 0..R-1");
+        key[m] = group[m] * R + dst[m];
+    }
+    std::vector<int64_t> order(n);
+    for (int64_t m = 0; m < n; ++m) order[m] = m;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return key[a] < key[b]; });
+    std::vector<int64_t> keys, off;
+    for (int64_t m = 0; m < n; ++m) {
+        if (m == 0 || key[order[m]] != key[order[m - 1]]) { keys.push_back(key[order[m]]); off.push_back(m); }
+    }
+    off.push_back(n);
+    const int nk = (int)keys.size();
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t b_keys = nk * 8, b_off = (nk + 1) * 8, b_ord = n * 8, b_req = n * req_sz, b_resp = n * resp_sz;
+    char* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, b_keys + b_off + b_ord + b_req + b_resp + 64));
+    char* pk = buf; char* po = pk + b_keys; char* pd = po + b_off; char* pq = pd + b_ord; char* ps = pq + b_req;
+    hipError_t err = hipMemcpyAsync(pk, keys.data(), b_keys, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(po, off.data(), b_off, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(pd, order.data(), b_ord, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(pq, req, b_req, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess) {
+        batch_kernel<<<(nk + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
+            e->S, e->dp, (uint32_t)e->t, kind, nk, (const int64_t*)pk, (const int64_t*)po, (const int64_t*)pd, pq,
+            resp_sz ? (void*)ps : nullptr);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess && resp_sz) err = hipMemcpyAsync(resp, ps, b_resp, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
+int raft_vote_batch(raft_engine* e, const int64_t* group, const int32_t* dst, const raft_vote_req* req,
+                    raft_vote_resp* resp, int64_t n) {
+    return run_batch(e, BATCH_VOTE, group, dst, req, sizeof(raft_vote_req), resp, sizeof(raft_vote_resp), n);
+}
+
+int raft_append_batch(raft_engine* e, const int64_t* group, const int32_t* dst, const raft_append_req* req,
+                      raft_append_resp* resp, int64_t n) {
+    return run_batch(e, BATCH_APPEND, group, dst, req, sizeof(raft_append_req), resp, sizeof(raft_append_resp), n);
+}
+
+int raft_append_command_batch(raft_engine* e, const int64_t* group, const int32_t* replica, const uint32_t* cmd,
+                              int64_t n) {
+    return run_batch(e, BATCH_COMMAND, group, replica, cmd, sizeof(uint32_t), nullptr, 0, n);
+}
+
+}  // extern "C"

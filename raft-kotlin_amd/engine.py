@@ -1,0 +1,175 @@
+"""RaftEngine — host-side handle of the HIP batched Raft engine (C-ABI in include/raft_engine.h).
+
+One engine owns G groups x R replicas of Raft node state in the HBM of one
+GPU.  ``step(n)`` advances every group by n lockstep heartbeat periods, which
+is what each reference node does on its own timers
+(RaftServer.kt:109-226, Commons.kt:10-31); the handler batches are the
+reference's gRPC service (RaftServer.vote / RaftServer.append,
+RaftServer.kt:228-287) applied to chosen replicas.
+
+There is no CPU fallback anywhere in this module: every call goes to the HIP
+library and a missing library or device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class RaftError(RuntimeError):
+    pass
+
+
+class RaftEngine:
+    def __init__(self, params: abi.raft_params, device: int = 0):
+        self._lib = abi.load_library()
+        self.p = params
+        self.R = int(params.R)
+        self.G = int(params.G)
+        self.g0 = int(params.g0)
+        self.cap = int(params.log_cap)
+        self.W = abi.group_words(self.R)
+        self.device = device
+        h = C.c_void_p()
+        self._check(self._lib.raft_engine_create(C.byref(params), device, C.byref(h)), "raft_engine_create")
+        self._h = h
+
+    # -- plumbing ---------------------------------------------------------
+    def _check(self, rc: int, what: str):
+        if rc != abi.RAFT_OK:
+            msg = self._lib.raft_last_error().decode(errors="replace")
+            raise RaftError(f"{what} failed ({rc}): {msg}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.raft_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def stream(self) -> int:
+        """hipStream_t of the engine (for torch.cuda.ExternalStream / events)."""
+        return int(self._lib.raft_engine_stream(self._h) or 0)
+
+    @property
+    def step_index(self) -> int:
+        return int(self._lib.raft_engine_step_index(self._h))
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self._lib.raft_engine_device_bytes(self._h))
+
+    # -- the hot path -----------------------------------------------------
+    def step(self, n: int = 1, counters: bool = True) -> np.ndarray | None:
+        """Advance n lockstep steps; returns [n, NUM_COUNTERS] int64 counters."""
+        c = abi.counters_array(n) if counters else None
+        self._check(self._lib.raft_engine_step(self._h, n, abi.ptr(c, C.c_int64) if c is not None else None),
+                    "raft_engine_step")
+        return c[:, : abi.NUM_COUNTERS] if c is not None else None
+
+    def step_async(self, n: int, counters_dev_ptr: int | None = None):
+        """Enqueue n steps on the engine stream; counters to a device buffer
+        of [n][COUNTER_STRIDE] int64 (e.g. a torch tensor's data_ptr())."""
+        self._check(self._lib.raft_engine_step_async(self._h, n, C.c_void_p(counters_dev_ptr or 0)),
+                    "raft_engine_step_async")
+
+    def set_kernel_timing(self, enable: bool = True):
+        """Bracket every step-kernel launch with HIP events on the engine stream."""
+        self._check(self._lib.raft_engine_set_kernel_timing(self._h, int(enable)), "set_kernel_timing")
+
+    def kernel_time(self):
+        """(summed step-kernel ms, launches) since the last call; synchronises."""
+        ms, n = C.c_double(), C.c_int64()
+        self._check(self._lib.raft_engine_kernel_time(self._h, C.byref(ms), C.byref(n)), "kernel_time")
+        return float(ms.value), int(n.value)
+
+    def sync(self):
+        self._check(self._lib.raft_engine_sync(self._h), "raft_engine_sync")
+
+    # -- state ------------------------------------------------------------
+    def read_state(self, g0: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.G - g0 if n is None else n
+        out = np.zeros((n, self.W), dtype=np.int32)
+        self._check(self._lib.raft_engine_read_state(self._h, g0, n, abi.ptr(out, C.c_int32)), "read_state")
+        return out
+
+    def write_state(self, state: np.ndarray, g0: int = 0):
+        s = np.ascontiguousarray(state, dtype=np.int32).reshape(-1, self.W)
+        self._check(self._lib.raft_engine_write_state(self._h, g0, s.shape[0], abi.ptr(s, C.c_int32)),
+                    "write_state")
+
+    def read_log(self, g0: int = 0, n: int | None = None):
+        n = self.G - g0 if n is None else n
+        t = np.zeros((n, self.R, self.cap), dtype=np.int32)
+        c = np.zeros((n, self.R, self.cap), dtype=np.uint32)
+        self._check(self._lib.raft_engine_read_log(self._h, g0, n, abi.ptr(t, C.c_int32), abi.ptr(c, C.c_uint32)),
+                    "read_log")
+        return t, c
+
+    def write_log(self, terms: np.ndarray, cmds: np.ndarray, g0: int = 0):
+        t = np.ascontiguousarray(terms, dtype=np.int32)
+        c = np.ascontiguousarray(cmds, dtype=np.uint32)
+        self._check(self._lib.raft_engine_write_log(self._h, g0, t.shape[0], abi.ptr(t, C.c_int32),
+                                                    abi.ptr(c, C.c_uint32)), "write_log")
+
+    def digest(self) -> int:
+        out = C.c_uint64()
+        self._check(self._lib.raft_engine_digest(self._h, C.byref(out)), "digest")
+        return int(out.value)
+
+    # -- the service boundary (RaftServer.kt:228-287, :100-107) -------------
+    def vote_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
+        """req: [n, 4] int32 (term, candidateId, lastLogIndex, lastLogTerm) ->
+        [n, 2] int32 (term, voteGranted)."""
+        g = np.ascontiguousarray(group, dtype=np.int64)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        q = np.ascontiguousarray(req, dtype=np.int32).reshape(-1, 4)
+        out = np.zeros((q.shape[0], 2), dtype=np.int32)
+        self._check(self._lib.raft_vote_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
+                                              abi.ptr(q, abi.raft_vote_req), abi.ptr(out, abi.raft_vote_resp),
+                                              q.shape[0]), "raft_vote_batch")
+        return out
+
+    def append_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
+        """req: [n, 8] int32 (term, leaderId, prevLogIndex, prevLogTerm, hasEntry,
+        entryTerm, entryCmd(u32 bits), leaderCommit) -> [n, 3] (term, success, status)."""
+        g = np.ascontiguousarray(group, dtype=np.int64)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        q = np.ascontiguousarray(req).astype(np.int64).astype(np.uint32).view(np.int32).reshape(-1, 8)
+        out = np.zeros((q.shape[0], 3), dtype=np.int32)
+        self._check(self._lib.raft_append_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
+                                                abi.ptr(q, abi.raft_append_req), abi.ptr(out, abi.raft_append_resp),
+                                                q.shape[0]), "raft_append_batch")
+        return out
+
+    def append_command_batch(self, group, replica, cmd):
+        g = np.ascontiguousarray(group, dtype=np.int64)
+        r = np.ascontiguousarray(replica, dtype=np.int32)
+        c = np.ascontiguousarray(cmd, dtype=np.uint32)
+        self._check(self._lib.raft_append_command_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(r, C.c_int32),
+                                                        abi.ptr(c, C.c_uint32), c.shape[0]),
+                    "raft_append_command_batch")
+
+
+def philox4x32_10(ctr, key):
+    """The engine's Philox (host side of the shared header), for KAT checks."""
+    lib = abi.load_library()
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    out = (C.c_uint32 * 4)()
+    lib.raft_philox4x32_10(c, k, out)
+    return list(out)

@@ -1,0 +1,77 @@
+"""The C-ABI library: loads, exports every symbol include/raft_engine.h declares,
+reports a clean error without a GPU, and its host-side Philox matches the KATs.
+No compute runs here (CPU-only container)."""
+import ctypes as C
+import importlib
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from helpers import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "raft_engine.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(raft_[a-z0-9_]+)\s*\(", src)
+    return sorted(set(n for n in names if n != "raft_group_words"))   # static inline helper
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(abi.LIB_PATH):
+        importlib.import_module("raft-kotlin_amd.build").build()
+    return abi.load_library()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    decl = declared_functions()
+    assert set(decl) == set(abi.EXPORTED_SYMBOLS), set(decl) ^ set(abi.EXPORTED_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (raft_\w+)", out))
+    missing = [n for n in decl if n not in exported]
+    assert not missing, missing
+
+
+def test_library_is_gfx950(lib):
+    data = open(abi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data          # the embedded code-object bundle id
+
+
+def test_abi_version_and_defaults(lib):
+    assert lib.raft_abi_version() == 1
+    p = abi.raft_params()
+    lib.raft_params_default(C.byref(p))
+    for k, v in abi.DEFAULTS.items():
+        assert getattr(p, k) == v, k
+
+
+def test_engine_philox_matches_kats(lib):
+    eng = importlib.import_module("raft-kotlin_amd.engine")
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "philox_kat.json")))
+    for v in kat["vectors"]:
+        ctr = [int(x, 16) for x in v["ctr"]]
+        key = [int(x, 16) for x in v["key"]]
+        assert eng.philox4x32_10(ctr, key) == [int(x, 16) for x in v["out"]]
+
+
+def test_create_rejects_bad_params_before_touching_a_device(lib):
+    p = abi.make_params(R=9)
+    h = C.c_void_p()
+    assert lib.raft_engine_create(C.byref(p), 0, C.byref(h)) == abi.RAFT_EINVAL
+    assert b"R must be" in lib.raft_last_error()
+
+
+def test_create_without_gpu_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    eng = importlib.import_module("raft-kotlin_amd.engine")
+    with pytest.raises(eng.RaftError):
+        eng.RaftEngine(abi.make_params(G=4))
