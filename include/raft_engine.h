@@ -200,6 +200,9 @@ void*   raft_engine_stream(raft_engine* e);
 int raft_engine_set_kernel_timing(raft_engine* e, int enable);
 int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches);
 int64_t raft_engine_step_index(raft_engine* e);   /* steps executed so far */
+/* Set the index of the next step (its Philox counter c0); with write_state
+ * this resumes a run exported at any step. */
+int     raft_engine_set_step_index(raft_engine* e, int64_t t);
 int64_t raft_engine_device_bytes(raft_engine* e); /* HBM owned by the engine */
 
 /* ---- state access (fixtures, parity) ----------------------------------- */

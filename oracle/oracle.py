@@ -43,6 +43,7 @@ def lib():
             "oracle_destroy": (None, [o]),
             "oracle_step": (C.c_int, [o, I32, P(I64), I32]),
             "oracle_step_index": (I64, [o]),
+            "oracle_set_step_index": (C.c_int, [o, I64]),
             "oracle_read_state": (C.c_int, [o, I64, I64, P(I32)]),
             "oracle_write_state": (C.c_int, [o, I64, I64, P(I32)]),
             "oracle_read_log": (C.c_int, [o, I64, I64, P(I32), P(U32)]),
@@ -147,6 +148,11 @@ class Oracle:
     @property
     def step_index(self):
         return lib().oracle_step_index(self.h)
+
+    @step_index.setter
+    def step_index(self, t):
+        if lib().oracle_set_step_index(self.h, int(t)) != 0:
+            raise ValueError(t)
 
     def read_state(self, g0=0, n=None):
         n = self.G - g0 if n is None else n

@@ -608,6 +608,11 @@ int oracle_step(oracle_t* o, int32_t n_steps, int64_t* counters, int32_t nthread
 }
 
 int64_t oracle_step_index(const oracle_t* o) { return o ? (int64_t)o->t : -1; }
+int oracle_set_step_index(oracle_t* o, int64_t t) {
+    if (!o || t < 0 || t > (int64_t)0xFFFFFFFFll) return RAFT_EINVAL;
+    o->t = (uint32_t)t;
+    return RAFT_OK;
+}
 
 /* ------------------------------------------------------------------ */
 /* canonical state export / import (include/raft_engine.h)             */

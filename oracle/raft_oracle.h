@@ -25,6 +25,7 @@ void oracle_destroy(oracle_t* o);
 /* counters: nullable [n_steps][RAFT_COUNTER_STRIDE]; nthreads <= 0 -> 1 */
 int  oracle_step(oracle_t* o, int32_t n_steps, int64_t* counters, int32_t nthreads);
 int64_t oracle_step_index(const oracle_t* o);
+int  oracle_set_step_index(oracle_t* o, int64_t t);
 int  oracle_read_state(const oracle_t* o, int64_t g0, int64_t n, int32_t* out);
 int  oracle_write_state(oracle_t* o, int64_t g0, int64_t n, const int32_t* in);
 int  oracle_read_log(const oracle_t* o, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds);

@@ -168,6 +168,7 @@ def load_library(path: str | None = None):
         "raft_engine_set_kernel_timing": (C.c_int, [eng, C.c_int]),
         "raft_engine_kernel_time": (C.c_int, [eng, P(C.c_double), P(I64)]),
         "raft_engine_step_index": (I64, [eng]),
+        "raft_engine_set_step_index": (C.c_int, [eng, I64]),
         "raft_engine_device_bytes": (I64, [eng]),
         "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
         "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
@@ -192,7 +193,7 @@ EXPORTED_SYMBOLS = [
     "raft_params_default", "raft_last_error", "raft_abi_version", "raft_engine_create",
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
-    "raft_engine_step_index", "raft_engine_device_bytes",
+    "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_philox4x32_10",

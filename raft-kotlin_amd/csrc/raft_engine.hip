@@ -59,7 +59,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // state <-> registers
 // ---------------------------------------------------------------------------
 template <int R>
-__device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64_t G, int64_t i, uint32_t& sess) {
+__device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64_t G, int64_t i) {
 #define LD(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -75,11 +75,11 @@ __device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64
         g.retry[r] = LD(RAFT_F_RETRY_MS, r);
     }
 #undef LD
-    sess = 0;
+    g.sdirty = 0;
 #pragma unroll
     for (int s = 0; s < R; ++s) {
         if (g.fl[s] & FL_HB) {
-            sess |= 1u << s;
+            g.sdirty |= 1u << s;
 #pragma unroll
             for (int d = 0; d < R; ++d) {
                 g.nx[s][d] = S.nx[((int64_t)s * R + d) * G + i];
@@ -95,7 +95,7 @@ __device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64
 }
 
 template <int R>
-__device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S, int64_t G, int64_t i, uint32_t sess) {
+__device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S, int64_t G, int64_t i) {
 #define ST(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -113,7 +113,7 @@ __device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S
 #undef ST
 #pragma unroll
     for (int s = 0; s < R; ++s) {
-        if ((sess >> s) & 1u) {
+        if ((g.sdirty >> s) & 1u) {
 #pragma unroll
             for (int d = 0; d < R; ++d) {
                 S.nx[((int64_t)s * R + d) * G + i] = g.nx[s][d];
@@ -162,8 +162,7 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, ui
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
     Group<R> g;
-    uint32_t sess = 0;
-    if (live) load_group<R>(g, S, p.G, i, sess);
+    if (live) load_group<R>(g, S, p.G, i);
     else {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -174,6 +173,7 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, ui
             for (int d = 0; d < R; ++d) g.nx[r][d] = g.mc[r][d] = 0;
         }
         g.iso = g.cmdc = 0;
+        g.sdirty = 0;
     }
     Stepper<R> st;
     for (int k = 0; k < nsteps; ++k) {
@@ -182,11 +182,7 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, ui
         for (int c = 0; c < NC; ++c) cnt[c] = 0;
         Ctx ctx{t0 + (uint32_t)k, (uint32_t)(p.g0 + i), -1, 0u,
                 p.log + (live ? i : 0) * (int64_t)R * p.cap, p.cap, cnt};
-        if (live) {
-            st.step(g, p, ctx);
-#pragma unroll
-            for (int s = 0; s < R; ++s) sess |= (g.fl[s] & FL_HB) ? (1u << s) : 0u;
-        }
+        if (live) st.step(g, p, ctx);
         // block partial of every counter for this step (no atomics: written, then reduced)
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -202,7 +198,7 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, ui
         }
         __syncthreads();
     }
-    if (live) store_group<R>(g, S, p.G, i, sess);
+    if (live) store_group<R>(g, S, p.G, i);
 }
 
 // counters[k][c] = sum over blocks of partials[k][b][c]   (grid = steps)
@@ -636,6 +632,11 @@ int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches)
     return RAFT_OK;
 }
 int64_t raft_engine_step_index(raft_engine* e) { return e ? (int64_t)e->t : -1; }
+int raft_engine_set_step_index(raft_engine* e, int64_t t) {
+    if (!e || t < 0 || t > (int64_t)0xFFFFFFFFll) return fail(RAFT_EINVAL, "bad step index");
+    e->t = (uint64_t)t;
+    return RAFT_OK;
+}
 int64_t raft_engine_device_bytes(raft_engine* e) { return e ? (int64_t)e->bytes : -1; }
 
 static int check_range(raft_engine* e, int64_t g0, int64_t n) {

@@ -166,6 +166,7 @@ struct Group {
     uint32_t fl[R];
     int32_t nx[R][R], mc[R][R];     // leader session of replica s: [s][d]
     int32_t iso, cmdc;              // harness: isolation word, commands issued
+    uint32_t sdirty;                // sessions to write back: active at load or started since
 
     __device__ __forceinline__ Rep rep(int r) {
         return Rep{term[r], voted[r], role[r], commit[r], last[r], phys[r], elec[r], phase[r], retry[r], fl[r]};
@@ -224,8 +225,11 @@ struct Stepper {
     }
 
     // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113), S-8
+    // (a session can start and end in one step: a stale leader ticking earlier
+    //  in phase A deposes the new one, Q3; its arrays still persist, S-8)
     __device__ __forceinline__ static void start_session(Group<R>& g, const Ctx& c, int r) {
         g.fl[r] |= FL_HB;
+        g.sdirty |= 1u << r;
 #pragma unroll
         for (int d = 0; d < R; ++d) { g.nx[r][d] = g.commit[r] + 1; g.mc[r][d] = 0; }
         c.cnt[RAFT_C_LEADERS_ELECTED]++;

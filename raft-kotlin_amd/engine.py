@@ -69,6 +69,10 @@ class RaftEngine:
     def step_index(self) -> int:
         return int(self._lib.raft_engine_step_index(self._h))
 
+    @step_index.setter
+    def step_index(self, t: int):
+        self._check(self._lib.raft_engine_set_step_index(self._h, int(t)), "set_step_index")
+
     @property
     def device_bytes(self) -> int:
         return int(self._lib.raft_engine_device_bytes(self._h))

@@ -40,8 +40,11 @@ def run_lockstep(e, o, steps, chunk, label, digest_every=1):
             raise AssertionError(f"{label}: counters differ at step {done + bad[0]} "
                                  f"({abi.COUNTER_NAMES[bad[1]]}): {ce[tuple(bad)]} vs {co[tuple(bad)]}")
         done += k
-        if digest_every and (done // chunk) % digest_every == 0:
-            assert e.digest() == o.digest(), f"{label}: digest differs after step {done}"
+        if digest_every and (done // chunk) % digest_every == 0 and e.digest() != o.digest():
+            se, so = e.read_state(), o.read_state()
+            assert_same_state(se, so, e.R, f"{label} @ step {done}")
+            assert_same_logs(se, e.read_log(), o.read_log(), e.R, f"{label} @ step {done}")
+            raise AssertionError(f"{label}: digest differs after step {done} with equal state and logs")
     se, so = e.read_state(), o.read_state()
     assert_same_state(se, so, e.R, label)
     assert_same_logs(se, e.read_log(), o.read_log(), e.R, label)
@@ -241,6 +244,26 @@ def test_kats_on_engine():
     e.step(1)
     s = e.read_state()[0]
     t, c = e.read_log()
-    assert fld(s, R, 0, "commit") == 1
+    assert fld(s, R, 0, "commit") == 2          # tick 3: all three ack the stale slot `b`
     for r in (1, 2):
         assert fld(s, R, r, "last") == 2 and [int(c[0, r, j]) for j in range(2)] == [a, b]
+
+
+def test_session_started_and_deposed_in_one_step():
+    """Regression: global group 53 of this config, step 13.  The candidate in
+    backoff wins its round (phase D starts its session), then the stale leader
+    with the lower replica index ticks first in phase A and deposes it (Q3);
+    the new session's nextIndex row must still persist (S-8)."""
+    kw = dict(R=3, G=1, g0=53, seed=103, log_cap=300, drop_ppm=100_000, churn_ppm=20_000, churn_steps=15,
+              cmd_ppm=500_000, partition_period=40, partition_len=10)
+    o = O.Oracle(abi.make_params(**kw))
+    o.step(12)
+    e = RaftEngine(abi.make_params(**kw))
+    e.write_state(o.read_state())
+    e.write_log(*o.read_log())
+    e.step_index = 12
+    o.step(1)
+    e.step(1)
+    s = o.read_state()[0]
+    assert session(s, 3, 2)[0] == [1, 1, 1] and not (fld(s, 3, 2, "flags") & abi.FL_HB_ACTIVE)
+    assert_same_state(e.read_state(), o.read_state(), 3, "group 53 step 13")
