@@ -194,28 +194,35 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, ui
             int v = 0;
 #pragma unroll
             for (int w = 0; w < WAVES_PER_BLOCK; ++w) v += red[w][threadIdx.x];
-            partials[((int64_t)k * gridDim.x + blockIdx.x) * NC + threadIdx.x] = v;
+            partials[((int64_t)k * NC + threadIdx.x) * gridDim.x + blockIdx.x] = v;
         }
         __syncthreads();
     }
     if (live) store_group<R>(g, S, p.G, i);
 }
 
-// counters[k][c] = sum over blocks of partials[k][b][c]   (grid = steps)
+// counters[k][c] = sum over blocks b of partials[k][c][b]: one workgroup per
+// (step, counter), a contiguous strided sweep + wave/LDS tree.
 __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const int32_t* __restrict__ partials, int nblocks,
                                                                 int64_t* __restrict__ counters) {
-    __shared__ int64_t acc[BLOCK];
-    const int k = blockIdx.x;
-    const int c = threadIdx.x % 32, part = threadIdx.x / 32;   // 8 partial sums per counter
+    __shared__ int64_t acc[WAVES_PER_BLOCK];
+    const int k = blockIdx.x / RAFT_COUNTER_STRIDE, c = blockIdx.x % RAFT_COUNTER_STRIDE;
     int64_t v = 0;
-    if (c < NC)
-        for (int b = part; b < nblocks; b += BLOCK / 32) v += partials[((int64_t)k * nblocks + b) * NC + c];
-    acc[threadIdx.x] = v;
+    if (c < NC) {
+        const int32_t* src = partials + ((int64_t)k * NC + c) * nblocks;
+        for (int b = threadIdx.x; b < nblocks; b += BLOCK) v += src[b];
+    }
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)((uint64_t)v >> 32);
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t s = ((uint64_t)hi << 32 | lo) + ((uint64_t)__shfl_xor(hi, o, 64) << 32 | __shfl_xor(lo, o, 64));
+        lo = (uint32_t)s; hi = (uint32_t)(s >> 32);
+    }
+    if ((threadIdx.x & 63) == 0) acc[threadIdx.x >> 6] = (int64_t)((uint64_t)hi << 32 | lo);
     __syncthreads();
-    if (threadIdx.x < RAFT_COUNTER_STRIDE) {
+    if (threadIdx.x == 0) {
         int64_t s = 0;
-        for (int q = 0; q < BLOCK / 32; ++q) s += acc[q * 32 + threadIdx.x];
-        counters[(int64_t)k * RAFT_COUNTER_STRIDE + threadIdx.x] = threadIdx.x < NC ? s : 0;
+        for (int w = 0; w < WAVES_PER_BLOCK; ++w) s += acc[w];
+        counters[(int64_t)k * RAFT_COUNTER_STRIDE + c] = s;
     }
 }
 
@@ -578,7 +585,7 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
             e->ev_used += 2;
         }
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
-        reduce_counters_kernel<<<k, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, dst);
+        reduce_counters_kernel<<<k * RAFT_COUNTER_STRIDE, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, dst);
         done += k;
     }
     HIP_TRY(hipGetLastError());
