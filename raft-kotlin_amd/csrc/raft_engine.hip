@@ -59,7 +59,8 @@ __device__ __forceinline__ int wave_sum(int v) {
 // state <-> registers
 // ---------------------------------------------------------------------------
 template <int R>
-__device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64_t G, int64_t i) {
+__device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, const DevParams& p, int64_t i) {
+    const int64_t G = p.G;
 #define LD(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -75,27 +76,21 @@ __device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, int64
         g.retry[r] = LD(RAFT_F_RETRY_MS, r);
     }
 #undef LD
-    g.sdirty = 0;
+    // the lowest active leader session becomes the register-resident primary
+    int s0 = -1;
 #pragma unroll
-    for (int s = 0; s < R; ++s) {
-        if (g.fl[s] & FL_HB) {
-            g.sdirty |= 1u << s;
+    for (int r = R - 1; r >= 0; --r) if (g.fl[r] & FL_HB) s0 = r;
+    g.s0 = -1;
 #pragma unroll
-            for (int d = 0; d < R; ++d) {
-                g.nx[s][d] = S.nx[((int64_t)s * R + d) * G + i];
-                g.mc[s][d] = S.mt[((int64_t)s * R + d) * G + i];
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < R; ++d) { g.nx[s][d] = 0; g.mc[s][d] = 0; }
-        }
-    }
+    for (int d = 0; d < R; ++d) { g.nx0[d] = 0; g.mc0[d] = 0; }
+    if (s0 >= 0) session_load<R>(g, p, i, s0);
     g.iso = S.gx[i];
     g.cmdc = S.gx[G + i];
 }
 
 template <int R>
-__device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S, int64_t G, int64_t i) {
+__device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S, const DevParams& p, int64_t i) {
+    const int64_t G = p.G;
 #define ST(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -111,16 +106,7 @@ __device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S
         ST(RAFT_F_RETRY_MS, r) = g.retry[r];
     }
 #undef ST
-#pragma unroll
-    for (int s = 0; s < R; ++s) {
-        if ((g.sdirty >> s) & 1u) {
-#pragma unroll
-            for (int d = 0; d < R; ++d) {
-                S.nx[((int64_t)s * R + d) * G + i] = g.nx[s][d];
-                S.mt[((int64_t)s * R + d) * G + i] = g.mc[s][d];
-            }
-        }
-    }
+    if (g.s0 >= 0) session_store<R>(g, p, i);
     S.gx[i] = g.iso;
     S.gx[G + i] = g.cmdc;
 }
@@ -156,49 +142,37 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevState S, DevParams p) {
 template <int R>
 __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, uint32_t t0, int nsteps,
                                                      int32_t* __restrict__ partials) {
-    __shared__ int red[WAVES_PER_BLOCK][NC];
+    __shared__ uint32_t red[WAVES_PER_BLOCK][NCW];
     const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < p.G;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
     Group<R> g;
-    if (live) load_group<R>(g, S, p.G, i);
-    else {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            g.term[r] = g.voted[r] = g.role[r] = g.commit[r] = g.last[r] = g.phys[r] = 0;
-            g.elec[r] = g.phase[r] = g.retry[r] = 0;
-            g.fl[r] = 0;
-#pragma unroll
-            for (int d = 0; d < R; ++d) g.nx[r][d] = g.mc[r][d] = 0;
-        }
-        g.iso = g.cmdc = 0;
-        g.sdirty = 0;
-    }
+    if (live) load_group<R>(g, S, p, i);
     Stepper<R> st;
     for (int k = 0; k < nsteps; ++k) {
-        int cnt[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) cnt[c] = 0;
-        Ctx ctx{t0 + (uint32_t)k, (uint32_t)(p.g0 + i), -1, 0u,
-                p.log + (live ? i : 0) * (int64_t)R * p.cap, p.cap, cnt};
+        Counters cnt;
+        cnt.clear();
+        Ctx ctx{t0 + (uint32_t)k, (uint32_t)(p.g0 + i), i, -1, 0u,
+                p.log + (live ? i : 0) * (int64_t)R * p.cap, p.cap, &cnt};
         if (live) st.step(g, p, ctx);
         // block partial of every counter for this step (no atomics: written, then reduced)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const int v = wave_sum(cnt[c]);
+        for (int c = 0; c < NCW; ++c) {
+            const uint32_t v = __ockl_wfred_add_u32(cnt.w[c]);
             if (lane == 0) red[wave][c] = v;
         }
         __syncthreads();
         if (threadIdx.x < NC) {
-            int v = 0;
+            const int c = threadIdx.x;
+            uint32_t v = 0;
 #pragma unroll
-            for (int w = 0; w < WAVES_PER_BLOCK; ++w) v += red[w][threadIdx.x];
-            partials[((int64_t)k * NC + threadIdx.x) * gridDim.x + blockIdx.x] = v;
+            for (int w = 0; w < WAVES_PER_BLOCK; ++w) v += (red[w][c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+            partials[((int64_t)k * NC + c) * gridDim.x + blockIdx.x] = (int32_t)v;
         }
         __syncthreads();
     }
-    if (live) store_group<R>(g, S, p.G, i);
+    if (live) store_group<R>(g, S, p, i);
 }
 
 // counters[k][c] = sum over blocks b of partials[k][c][b]: one workgroup per
@@ -357,7 +331,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevState S, DevParams p, u
     RepState x;
     load_rep(x, S, R, p.G, i, r);
     uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
-    int cnt[NC];
+    Counters cnt;
+    cnt.clear();
     for (int m = off[k]; m < off[k + 1]; ++m) {
         const int64_t o = order[m];
         if (kind == BATCH_VOTE) {
@@ -540,6 +515,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->counters_dev = (int64_t*)b; b += al(cnt_b);
     e->S.log = (uint2*)b;
     d.log = e->S.log;
+    d.nx = e->S.nx;
+    d.mt = e->S.mt;
     *out = e;
     dispatch_R<InitL>(p->R, e);
     err = hipStreamSynchronize(e->stream);

@@ -1,14 +1,20 @@
 // raft_step.h — the per-node consensus step of arodionov/raft-kotlin as
 // register-resident SIMT code for gfx950.
 //
-// One lane owns one Raft group: all R replicas' scalar state, their leader
-// sessions (nextIndex/matchIndex) and the step's message temporaries live in
-// VGPRs.  Every loop over replicas is unrolled against the compile-time R, so
-// the R x R request/response "message tensor" of a phase never exists in
-// memory: a message is a handler call whose arguments are registers of the
-// sender and whose effects land in registers of the receiver.  Only the logs
-// (the reference's ArrayList, Commons.kt:51) stay in HBM, touched at the
-// slots the handlers read or write.
+// One lane owns one Raft group: all R replicas' scalar state, the group's
+// primary leader session (nextIndex/matchIndex of one leader) and the step's
+// message temporaries live in VGPRs; replica loops are unrolled against the
+// compile-time R, so the R x R request/response "message tensor" of a phase
+// never exists in memory: a message is a handler call whose arguments are
+// registers of the sender and whose effects land in registers of the
+// receiver.  The logs (the reference's ArrayList, Commons.kt:51) stay in HBM
+// and are touched only at the slots the handlers read or write.
+//
+// Leader ticks (phase A) iterate only the lane's *active* sessions (one, in
+// steady state) with the leader index as a per-lane runtime value; the
+// leader's scalars are picked with select chains and the destination loop
+// stays unrolled.  Sessions other than the primary live in their canonical
+// HBM rows and are swapped in when they tick (partitions, stale leaders).
 //
 // The phase order and every tie-break follow DESIGN.md §3 (the same schedule
 // the CPU oracle in oracle/raft_oracle.c restates object by object).
@@ -17,9 +23,12 @@
 #include "philox.h"
 #include "../../include/raft_engine.h"
 
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
+
 namespace raft {
 
 constexpr int NC = RAFT_NUM_COUNTERS;
+constexpr int NCW = (NC + 1) / 2;          // counters packed as 16-bit pairs per lane
 
 // exported flag bits (include/raft_engine.h) and engine-internal ones
 constexpr uint32_t FL_ARMED = RAFT_FL_ARMED;
@@ -33,6 +42,8 @@ constexpr int PEND_SH = RAFT_FL_PENDING_SHIFT, VOTES_SH = RAFT_FL_VOTES_SHIFT, L
 
 struct DevParams {
     uint2* log;                                // [G][R][cap] (term, cmd)
+    int32_t* nx;                               // [R][R][G] session rows (canonical home)
+    int32_t* mt;                               // [R][R][G]
     int64_t G, g0;
     int32_t R, cap;
     uint32_t key0, key1;
@@ -45,6 +56,18 @@ struct DevParams {
 
 struct Entry { int32_t term; uint32_t cmd; };
 
+// Per-lane step counters, two 16-bit counters per register (a lane's count in
+// one step is far below 2^16 / 64, so a wave sum of a packed word cannot
+// carry between halves).
+struct Counters {
+    uint32_t w[NCW];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int i = 0; i < NCW; ++i) w[i] = 0;
+    }
+    __device__ __forceinline__ void add(int c, uint32_t v = 1) { w[c >> 1] += v << (16 * (c & 1)); }
+};
+
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
     return philox4x32_10(c0, gid, purpose, sub, p.key0, p.key1);
 }
@@ -52,11 +75,12 @@ __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t 
 // Per-(group, step) context.
 struct Ctx {
     uint32_t t, gid;
+    int64_t i;            // engine-local group index (lane)
     int32_t iso;          // isolated replica this step, -1 if none
     uint32_t part;        // replicas on side B of this step's partition
     uint2* lg;            // this group's log, [R][cap] entries (term, cmd)
     int cap;
-    int* cnt;             // this lane's counters for the step
+    Counters* cnt;        // this lane's counters for the step
 };
 
 // One replica's scalar state, by reference into the owning lane's registers.
@@ -64,6 +88,26 @@ struct Rep {
     int32_t &term, &voted, &role, &commit, &last, &phys, &elec, &phase, &retry;
     uint32_t& fl;
 };
+
+// Pick / replace element s of a register array for a per-lane runtime s,
+// given as the one-hot mask 1 << s.  Written as masked OR / blend so the
+// optimiser cannot turn it into a dynamically indexed load or store (which
+// would demote the whole register array to scratch memory).
+template <int R>
+__device__ __forceinline__ int32_t pick(const int32_t (&a)[R], uint32_t onehot) {
+    int32_t v = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v |= a[r] & -(int32_t)((onehot >> r) & 1u);
+    return v;
+}
+template <int R>
+__device__ __forceinline__ void place(int32_t (&a)[R], uint32_t onehot, int32_t v) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int32_t m = -(int32_t)((onehot >> r) & 1u);
+        a[r] = (a[r] & ~m) | (v & m);
+    }
+}
 
 // ---- timer / consumer (Commons.kt:10-31, RaftServer.kt:50-69) -------------
 // reset(): re-arm with a fresh draw.  The draw is a pure function of
@@ -73,10 +117,6 @@ __device__ __forceinline__ void reset_timer(Rep n) { n.fl |= FL_ARMED | FL_DRAW;
 // launch { channel.send(FOLLOWER) } (RaftServer.kt:241, :261, :266), S-5
 __device__ __forceinline__ void send_follower(Rep n) {
     if (n.fl & FL_ELECTING) n.fl |= FL_PRST; else reset_timer(n);
-}
-// channel.offer(FOLLOWER) (RaftServer.kt:152), S-6
-__device__ __forceinline__ void offer_follower(Rep n) {
-    if (!(n.fl & FL_ELECTING)) reset_timer(n);
 }
 
 // ---- Log<T> (Commons.kt:47-74) over one replica's HBM slots ---------------
@@ -98,14 +138,14 @@ __device__ __forceinline__ int log_add(uint2* lr, int cap, int32_t& last, int32_
 
 // ---- vote() (RaftServer.kt:228-251) ---------------------------------------
 __device__ __forceinline__ void vote_handler(Rep n, const uint2* lr, int32_t rt, int32_t rc, int32_t rli,
-                                             int32_t rlt, int* cnt, int32_t& resp_term, bool& granted) {
+                                             int32_t rlt, Counters& cnt, int32_t& resp_term, bool& granted) {
     granted = false;
     if (rt < n.term) {
     } else if (n.term == rt) {
         granted = n.voted == rc;
     } else {
         int32_t lt = 0;
-        if (n.last >= 1) { lt = (int32_t)lr[n.last - 1].x; cnt[RAFT_C_VOTE_LOG_READS]++; }
+        if (n.last >= 1) { lt = (int32_t)lr[n.last - 1].x; cnt.add(RAFT_C_VOTE_LOG_READS); }
         if (n.last >= 1 && rlt < lt) {
         } else if (n.last >= 1 && rlt == lt && rli < n.last) {
         } else {
@@ -114,14 +154,14 @@ __device__ __forceinline__ void vote_handler(Rep n, const uint2* lr, int32_t rt,
             granted = true;
         }
     }
-    if (granted) cnt[RAFT_C_VOTES_GRANTED]++;
+    if (granted) cnt.add(RAFT_C_VOTES_GRANTED);
     resp_term = n.term;
 }
 
 // ---- append() (RaftServer.kt:253-287); returns false where it throws -------
 __device__ __forceinline__ bool append_handler(Rep n, int32_t id, uint2* lr, int cap, int32_t rt, int32_t rlead,
                                                int32_t prev, int32_t prevTerm, bool has, Entry e,
-                                               int32_t lcommit, int* cnt, int32_t& resp_term, bool& success) {
+                                               int32_t lcommit, Counters& cnt, int32_t& resp_term, bool& success) {
     if (rt > n.term) {                                  // :257-262
         n.term = rt; n.voted = -1; n.role = RAFT_FOLLOWER;
         send_follower(n);
@@ -132,29 +172,29 @@ __device__ __forceinline__ bool append_handler(Rep n, int32_t id, uint2* lr, int
     }
     if (lcommit > n.commit) {                           // :270-272 (Q4)
         const int32_t c = min(lcommit, n.last);
-        if (c < n.commit) cnt[RAFT_C_COMMIT_REGRESSIONS]++;
+        if (c < n.commit) cnt.add(RAFT_C_COMMIT_REGRESSIONS);
         n.commit = c;
     }
     if (prev == -1) success = true;                     // :274-276
     else if (n.last > prev) {
         if (prev < 0) { resp_term = n.term; success = false; return false; }
-        cnt[RAFT_C_PREV_READS_FOLLOWER]++;
+        cnt.add(RAFT_C_PREV_READS_FOLLOWER);
         success = (int32_t)lr[prev].x == prevTerm;
     } else success = false;
     if (success && has) {                               // :278 (Q2, Q10)
         const int r = log_add(lr, cap, n.last, n.phys, prev + 1, e);
-        if (r == 1) cnt[RAFT_C_ENTRY_WRITES]++;
-        else if (r == -1) cnt[RAFT_C_LOG_OVERFLOW]++;
+        if (r == 1) cnt.add(RAFT_C_ENTRY_WRITES);
+        else if (r == -1) cnt.add(RAFT_C_LOG_OVERFLOW);
     }
     resp_term = n.term;
     return true;
 }
 
 // ---- appendCommand() (RaftServer.kt:100-107) ------------------------------
-__device__ __forceinline__ void append_command(Rep n, uint2* lr, int cap, uint32_t cmd, int* cnt) {
+__device__ __forceinline__ void append_command(Rep n, uint2* lr, int cap, uint32_t cmd, Counters& cnt) {
     const int r = log_add(lr, cap, n.last, n.phys, n.last, Entry{n.term, cmd});
-    cnt[RAFT_C_COMMANDS]++;
-    if (r == -1) cnt[RAFT_C_LOG_OVERFLOW]++;
+    cnt.add(RAFT_C_COMMANDS);
+    if (r == -1) cnt.add(RAFT_C_LOG_OVERFLOW);
 }
 
 // ---------------------------------------------------------------------------
@@ -164,14 +204,33 @@ template <int R>
 struct Group {
     int32_t term[R], voted[R], role[R], commit[R], last[R], phys[R], elec[R], phase[R], retry[R];
     uint32_t fl[R];
-    int32_t nx[R][R], mc[R][R];     // leader session of replica s: [s][d]
+    int32_t s0;                     // owner of the primary session in registers, -1 none
+    int32_t nx0[R], mc0[R];         // its nextIndex / matchIndex (RaftServer.kt:112-113)
     int32_t iso, cmdc;              // harness: isolation word, commands issued
-    uint32_t sdirty;                // sessions to write back: active at load or started since
 
     __device__ __forceinline__ Rep rep(int r) {
         return Rep{term[r], voted[r], role[r], commit[r], last[r], phys[r], elec[r], phase[r], retry[r], fl[r]};
     }
 };
+
+// primary-session spill / fill (canonical HBM rows nx/mt[s][d][G])
+template <int R>
+__device__ __forceinline__ void session_store(const Group<R>& g, const DevParams& p, int64_t i) {
+#pragma unroll
+    for (int d = 0; d < R; ++d) {
+        p.nx[((int64_t)g.s0 * R + d) * p.G + i] = g.nx0[d];
+        p.mt[((int64_t)g.s0 * R + d) * p.G + i] = g.mc0[d];
+    }
+}
+template <int R>
+__device__ __forceinline__ void session_load(Group<R>& g, const DevParams& p, int64_t i, int s) {
+    g.s0 = s;
+#pragma unroll
+    for (int d = 0; d < R; ++d) {
+        g.nx0[d] = p.nx[((int64_t)s * R + d) * p.G + i];
+        g.mc0[d] = p.mt[((int64_t)s * R + d) * p.G + i];
+    }
+}
 
 template <int R>
 struct Stepper {
@@ -182,14 +241,21 @@ struct Stepper {
     int32_t qt[R], qli[R], qlt[R];
     uint32_t send[R];
 
+    // 16-bit drop uniform j = 2*dd + b of sender s (S-9); s may be a runtime value
     __device__ __forceinline__ static bool lost(const DevParams& p, const Ctx& c, const u32x4* du, int s, int d, int b) {
         if (s == d) return false;                                      // S-7
         if (c.iso >= 0 && (s == c.iso || d == c.iso)) return true;
         if (((c.part >> s) ^ (c.part >> d)) & 1u) return true;
         if (p.drop_thr16 == 0) return false;
         const int dd = d < s ? d : d - 1;
-        const int j = 2 * dd + b;
-        const uint32_t word = word_of(du[j >> 3], (j & 7) >> 1);
+        const int j = 2 * dd + b;                   // 0 .. 2R-3 < 16
+        // word j >> 1 of the 8-word (du[0], du[1]) pair, by one-hot masks (no
+        // dynamic indexing: it would demote du to scratch)
+        const uint32_t oh = 1u << (j >> 1);
+        const uint32_t w8[8] = {du[0].x, du[0].y, du[0].z, du[0].w, du[1].x, du[1].y, du[1].z, du[1].w};
+        uint32_t word = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) word |= w8[k] & (0u - ((oh >> k) & 1u));
         return ((word >> (16 * (j & 1))) & 0xFFFFu) < p.drop_thr16;
     }
 
@@ -207,7 +273,7 @@ struct Stepper {
         else {
             const uint2* lr = c.lg + r * c.cap;
             qlt[r] = (int32_t)lr[g.last[r] - 1].x;
-            c.cnt[RAFT_C_VOTE_LOG_READS]++;
+            c.cnt->add(RAFT_C_VOTE_LOG_READS);
         }
     }
 
@@ -221,22 +287,22 @@ struct Stepper {
         g.retry[r] = 0;
         send[r] = ALL;
         build_vote_request(g, c, r);
-        c.cnt[RAFT_C_ROUNDS]++;
+        c.cnt->add(RAFT_C_ROUNDS);
     }
 
-    // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113), S-8
-    // (a session can start and end in one step: a stale leader ticking earlier
-    //  in phase A deposes the new one, Q3; its arrays still persist, S-8)
-    __device__ __forceinline__ static void start_session(Group<R>& g, const Ctx& c, int r) {
+    // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113), S-8.
+    // The primary slot is taken over; the previous owner's row goes home.
+    __device__ __forceinline__ static void start_session(Group<R>& g, const DevParams& p, const Ctx& c, int r) {
         g.fl[r] |= FL_HB;
-        g.sdirty |= 1u << r;
+        if (g.s0 >= 0 && g.s0 != r) session_store<R>(g, p, c.i);
+        g.s0 = r;
 #pragma unroll
-        for (int d = 0; d < R; ++d) { g.nx[r][d] = g.commit[r] + 1; g.mc[r][d] = 0; }
-        c.cnt[RAFT_C_LEADERS_ELECTED]++;
+        for (int d = 0; d < R; ++d) { g.nx0[d] = g.commit[r] + 1; g.mc0[d] = 0; }
+        c.cnt->add(RAFT_C_LEADERS_ELECTED);
     }
 
     // leaderElection() returns; queued sends then the final state (S-5)
-    __device__ __forceinline__ static void end_election(Group<R>& g, const Ctx& c, int r) {
+    __device__ __forceinline__ static void end_election(Group<R>& g, const DevParams& p, const Ctx& c, int r) {
         uint32_t f = g.fl[r];
         const bool prst = f & FL_PRST;
         f &= ~(FL_ELECTING | FL_PRST | FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH));
@@ -244,12 +310,103 @@ struct Stepper {
         g.fl[r] = f;
         g.phase[r] = 0;
         g.retry[r] = 0;
-        if (g.role[r] == RAFT_LEADER) start_session(g, c, r);                 // :66
-        else if (g.role[r] == RAFT_FOLLOWER) g.fl[r] |= FL_ARMED | FL_DRAW;   // :64
+        if (g.role[r] == RAFT_LEADER) start_session(g, p, c, r);             // :66
+        else if (g.role[r] == RAFT_FOLLOWER) g.fl[r] |= FL_ARMED | FL_DRAW;  // :64
+    }
+
+    // One fixedRateTimer tick of leader s (RaftServer.kt:115-176); s is a
+    // per-lane runtime index.  Requests are all built before any handler runs
+    // (S-4); responses are processed in dst order on a working copy of the
+    // leader's scalars, written back at the end.  The self-handler (d == s)
+    // only ever touches s's log, lastIndex and physLen (its request carries
+    // leaderId == id and the tick-start term and commit), so the copy and the
+    // registers never disagree on anything a handler reads.
+    __device__ __forceinline__ static void tick(Group<R>& g, const DevParams& p, Ctx& c, int s) {
+        Counters& cnt = *c.cnt;
+        const uint32_t oh = 1u << s;
+        if (pick(g.role, oh) == RAFT_FOLLOWER) {                      // :117 cancel() (S-10)
+#pragma unroll
+            for (int r = 0; r < R; ++r) g.fl[r] &= ~(((oh >> r) & 1u) * FL_HB);
+            return;
+        }
+        cnt.add(RAFT_C_SESSIONS_TICKED);
+        if (s != g.s0) {                                               // swap the session in
+            if (g.s0 >= 0) session_store<R>(g, p, c.i);
+            session_load<R>(g, p, c.i, s);
+        }
+        const int32_t Lterm = pick(g.term, oh), Lcommit = pick(g.commit, oh), Llast = pick(g.last, oh);
+        const uint2* ls = c.lg + s * c.cap;
+        // build every request first (RaftServer.kt:122-132)
+        uint32_t okm = 0, hasm = 0;
+        int32_t pvt[R];
+        Entry ent[R];
+#pragma unroll
+        for (int d = 0; d < R; ++d) {
+            const int32_t i = g.nx0[d], prev = i - 2;
+            bool ok = true;
+            pvt[d] = -1;
+            ent[d] = Entry{0, 0u};
+            if (prev >= 0) {                                           // :128 (Q11)
+                if (prev > Llast - 1) ok = false;
+                else { pvt[d] = (int32_t)ls[prev].x; cnt.add(RAFT_C_PREV_READS_LEADER); }
+            }
+            if (ok && Llast >= i) {                                    // :130-131
+                if (i - 1 < 0) ok = false;
+                else {
+                    const uint2 e = ls[i - 1];
+                    ent[d] = Entry{(int32_t)e.x, e.y};
+                    hasm |= 1u << d;
+                    cnt.add(RAFT_C_ENTRY_READS_LEADER);
+                }
+            }
+            if (ok) okm |= 1u << d;
+            else cnt.add(RAFT_C_APPEND_SKIPPED);
+        }
+        u32x4 du[2];
+        if (p.drop_thr16) drop_uniforms(p, c, RAFT_RNG_APPEND_DROP, s, du);
+        int32_t T = Lterm, C = Lcommit;
+        bool stepdown = false;
+#pragma unroll
+        for (int d = 0; d < R; ++d) {
+            if (!((okm >> d) & 1u)) continue;
+            cnt.add(RAFT_C_APPEND_SENT);
+            if (lost(p, c, du, s, d, 0)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }   // :170-172
+            const int32_t prev = g.nx0[d] - 2;
+            const bool has = (hasm >> d) & 1u;
+            int32_t rterm; bool succ;
+            if (!append_handler(g.rep(d), d + 1, c.lg + d * c.cap, c.cap, Lterm, s + 1, prev, pvt[d], has, ent[d],
+                                Lcommit, cnt, rterm, succ))
+                continue;
+            if (lost(p, c, du, s, d, 1)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
+            if (rterm > T) { T = rterm; stepdown = true; continue; }  // :146-154 (Q7)
+            if (succ) {                                                // :156-165 (Q9)
+                if (has) {
+                    g.nx0[d] += 1;
+                    g.mc0[d] += 1;
+                    cnt.add(RAFT_C_ENTRIES_ACKED);
+                    int k = 0;
+#pragma unroll
+                    for (int q = 0; q < R; ++q) k += g.mc0[q] > C;     // :161
+                    if (k >= MAJ) { C += 1; cnt.add(RAFT_C_COMMITS); } // :162
+                } else {
+                    g.mc0[d] = prev + 1;                               // :164
+                }
+            } else {
+                g.nx0[d] -= 1;                                         // :167
+            }
+        }
+        place(g.term, oh, T);
+        place(g.commit, oh, C);
+        if (stepdown) {                                                // :148 + offer(FOLLOWER) :152 (S-6)
+            place(g.role, stepdown ? oh : 0u, RAFT_FOLLOWER);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (((oh >> r) & 1u) && !(g.fl[r] & FL_ELECTING)) g.fl[r] |= FL_ARMED | FL_DRAW;
+        }
     }
 
     __device__ __forceinline__ void step(Group<R>& g, const DevParams& p, Ctx& c) {
-        int* cnt = c.cnt;
+        Counters& cnt = *c.cnt;
         // ---------------- H: harness ----------------
         u32x4 hw = u32x4{0u, 0u, 0u, 0u};
         if (p.churn_thr32 | p.cmd_thr32) hw = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
@@ -281,7 +438,7 @@ struct Stepper {
                 if (g.elec[r] <= 0) {                                   // Commons.kt:25-27
                     g.fl[r] &= ~FL_ARMED;
                     g.elec[r] = 0;
-                    cnt[RAFT_C_TIMEOUTS]++;
+                    cnt.add(RAFT_C_TIMEOUTS);
                     g.role[r] = RAFT_CANDIDATE;                         // RaftServer.kt:182
                     if (!(g.fl[r] & FL_ELECTING)) {                     // :184 -> :65
                         g.fl[r] |= FL_ELECTING;
@@ -302,7 +459,7 @@ struct Stepper {
                     g.phase[r] -= p.P;                                  // delay(backoff) :221
                     if (g.phase[r] <= 0) {
                         if (g.role[r] == RAFT_CANDIDATE) start_round(g, c, r);   // :191
-                        else end_election(g, c, r);
+                        else end_election(g, p, c, r);
                     }
                 }
             }
@@ -322,10 +479,10 @@ struct Stepper {
 #pragma unroll
                     for (int d = 0; d < R; ++d) {
                         if (!((send[s] >> d) & 1u)) continue;
-                        if (lost(p, c, du, s, d, 0)) { cnt[RAFT_C_MSG_DROPPED]++; continue; }
+                        if (lost(p, c, du, s, d, 0)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
                         int32_t rterm; bool granted;
                         vote_handler(g.rep(d), c.lg + d * c.cap, qt[s], s + 1, qli[s], qlt[s], cnt, rterm, granted);
-                        if (lost(p, c, du, s, d, 1)) { cnt[RAFT_C_MSG_DROPPED]++; continue; }
+                        if (lost(p, c, du, s, d, 1)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
                         uint32_t f = g.fl[s];
                         f &= ~(1u << (PEND_SH + d));
                         f += 1u << LATCH_SH;                              // :209
@@ -349,88 +506,26 @@ struct Stepper {
             g.fl[r] = f & ~(0xFFu << PEND_SH);                          // cancelChildren() :215
             if (g.role[r] == RAFT_CANDIDATE && votes >= MAJ) {          // :218-219
                 g.role[r] = RAFT_LEADER;
-                end_election(g, c, r);
+                end_election(g, p, c, r);
             } else if (g.role[r] == RAFT_CANDIDATE) {                   // :220-221
                 g.fl[r] = (g.fl[r] & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
                 const u32x4 w = draw(p, c.t, c.gid, RAFT_RNG_BACKOFF, (uint32_t)(r >> 2));
                 g.phase[r] = scale_range(word_of(w, r & 3), p.bmin, p.bmax);
                 g.retry[r] = 0;
             } else {
-                end_election(g, c, r);
+                end_election(g, p, c, r);
             }
         }
 
-        // ---------------- A: leader ticks (S-3, S-4) ----------------
+        // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
+        uint32_t todo = 0;
 #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            bool active = (g.fl[s] & FL_HB) != 0;
-            if (active && g.role[s] == RAFT_FOLLOWER) { g.fl[s] &= ~FL_HB; active = false; }   // :117 (S-10)
-            if (!__any(active)) continue;
-            if (active) {
-                cnt[RAFT_C_SESSIONS_TICKED]++;
-                // build every request first (RaftServer.kt:122-132)
-                const uint2* ls = c.lg + s * c.cap;
-                const int32_t sterm = g.term[s], scommit = g.commit[s], slast = g.last[s];
-                bool ok[R], has[R];
-                int32_t pv[R], pvt[R];
-                Entry ent[R];
-#pragma unroll
-                for (int d = 0; d < R; ++d) {
-                    const int32_t i = g.nx[s][d];
-                    pv[d] = i - 2;
-                    pvt[d] = -1;
-                    ok[d] = true;
-                    has[d] = false;
-                    ent[d] = Entry{0, 0u};
-                    if (pv[d] >= 0) {                                  // :128 (Q11)
-                        if (pv[d] > slast - 1) ok[d] = false;
-                        else { pvt[d] = (int32_t)ls[pv[d]].x; cnt[RAFT_C_PREV_READS_LEADER]++; }
-                    }
-                    if (ok[d] && slast >= i) {                          // :130-131
-                        if (i - 1 < 0) ok[d] = false;
-                        else {
-                            const uint2 e = ls[i - 1];
-                            ent[d] = Entry{(int32_t)e.x, e.y};
-                            has[d] = true;
-                            cnt[RAFT_C_ENTRY_READS_LEADER]++;
-                        }
-                    }
-                    if (!ok[d]) cnt[RAFT_C_APPEND_SKIPPED]++;
-                }
-                u32x4 du[2];
-                if (p.drop_thr16) drop_uniforms(p, c, RAFT_RNG_APPEND_DROP, s, du);
-#pragma unroll
-                for (int d = 0; d < R; ++d) {
-                    if (!ok[d]) continue;
-                    cnt[RAFT_C_APPEND_SENT]++;
-                    if (lost(p, c, du, s, d, 0)) { cnt[RAFT_C_MSG_DROPPED]++; continue; }   // :170-172
-                    int32_t rterm; bool succ;
-                    if (!append_handler(g.rep(d), d + 1, c.lg + d * c.cap, c.cap, sterm, s + 1, pv[d], pvt[d],
-                                        has[d], ent[d], scommit, cnt, rterm, succ))
-                        continue;
-                    if (lost(p, c, du, s, d, 1)) { cnt[RAFT_C_MSG_DROPPED]++; continue; }
-                    if (rterm > g.term[s]) {                            // :146-154 (Q7)
-                        g.term[s] = rterm;
-                        g.role[s] = RAFT_FOLLOWER;
-                        offer_follower(g.rep(s));
-                        continue;
-                    }
-                    if (succ) {                                         // :156-165 (Q9)
-                        if (has[d]) {
-                            g.nx[s][d] += 1;
-                            g.mc[s][d] += 1;
-                            cnt[RAFT_C_ENTRIES_ACKED]++;
-                            int k = 0;
-#pragma unroll
-                            for (int q = 0; q < R; ++q) k += g.mc[s][q] > g.commit[s];   // :161
-                            if (k >= MAJ) { g.commit[s] += 1; cnt[RAFT_C_COMMITS]++; }    // :162
-                        } else {
-                            g.mc[s][d] = pv[d] + 1;                     // :164
-                        }
-                    } else {
-                        g.nx[s][d] -= 1;                                // :167
-                    }
-                }
+        for (int r = 0; r < R; ++r) todo |= (g.fl[r] & FL_HB) ? (1u << r) : 0u;
+        while (__any(todo != 0)) {
+            if (todo != 0) {
+                const int s = __builtin_ctz(todo);
+                todo &= todo - 1u;
+                tick(g, p, c, s);
             }
         }
 
@@ -458,9 +553,9 @@ struct Stepper {
             for (int q = r + 1; q < R; ++q)
                 dual |= g.role[q] == RAFT_LEADER && g.term[q] == g.term[r];
         }
-        cnt[RAFT_C_LEADERS] += leaders;
-        cnt[RAFT_C_GROUPS_WITH_LEADER] += leaders > 0;
-        cnt[RAFT_C_DUAL_LEADER_GROUPS] += dual;
+        cnt.add(RAFT_C_LEADERS, (uint32_t)leaders);
+        if (leaders > 0) cnt.add(RAFT_C_GROUPS_WITH_LEADER);
+        if (dual) cnt.add(RAFT_C_DUAL_LEADER_GROUPS);
 
         resolve_timer_draws(g, p, c);
     }
