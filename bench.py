@@ -34,7 +34,7 @@ abi = importlib.import_module("raft-kotlin_amd.abi")
 
 METRIC = "Raft group-steps/sec (whole node) at 1M×5-replica groups; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-STATE_BYTES_PER_REPLICA = 4 * abi.NUM_FIELDS
+STATE_BYTES_PER_REPLICA = 4 * (abi.NUM_FIELDS + 3)   # 10 canonical fields + the log-tail cache (t1, t2, c1)
 GROUP_EXTRA_BYTES = 4 * abi.GROUP_EXTRA
 
 

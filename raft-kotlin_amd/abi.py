@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libraft_engine.so")
+# RAFT_ENGINE_LIB selects an alternative in-tree build (tuning experiments only)
+LIB_PATH = os.environ.get("RAFT_ENGINE_LIB") or os.path.join(PKG_DIR, "lib", "libraft_engine.so")
 
 RAFT_OK = 0
 RAFT_EINVAL = -1

@@ -2,7 +2,9 @@
 //
 // HBM layout (structure of arrays, lane = group, so every state access of a
 // wave is one contiguous 256-byte run per field):
-//   st  int32 [RAFT_NUM_FIELDS][R][G]     per-replica scalars (RaftServer.kt:35-48)
+//   st  int32 [F_DEV][R][G]               per-replica scalars (RaftServer.kt:35-48): the
+//                                         RAFT_NUM_FIELDS canonical ones, then the
+//                                         engine-internal log-tail cache (t1, t2, c1)
 //   nx  int32 [R][R][G]                   nextIndex  of replica s's session towards d
 //   mt  int32 [R][R][G]                   matchIndex (RaftServer.kt:112-113)
 //   gx  int32 [2][G]                      harness words (isolation, commands issued)
@@ -46,6 +48,8 @@ struct DevState {
     uint2* log;
 };
 
+constexpr int F_T1 = RAFT_NUM_FIELDS, F_T2 = RAFT_NUM_FIELDS + 1, F_C1 = RAFT_NUM_FIELDS + 2;
+constexpr int F_DEV = RAFT_NUM_FIELDS + 3;
 constexpr int BLOCK = 256;
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 
@@ -74,6 +78,9 @@ __device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, const
         g.fl[r] = (uint32_t)LD(RAFT_F_FLAGS, r);
         g.phase[r] = LD(RAFT_F_PHASE_MS, r);
         g.retry[r] = LD(RAFT_F_RETRY_MS, r);
+        g.t1[r] = LD(F_T1, r);
+        g.t2[r] = LD(F_T2, r);
+        g.c1[r] = (uint32_t)LD(F_C1, r);
     }
 #undef LD
     // the lowest active leader session becomes the register-resident primary
@@ -104,6 +111,9 @@ __device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S
         ST(RAFT_F_FLAGS, r) = (int32_t)(g.fl[r] & FL_EXPORT_MASK);
         ST(RAFT_F_PHASE_MS, r) = g.phase[r];
         ST(RAFT_F_RETRY_MS, r) = g.retry[r];
+        ST(F_T1, r) = g.t1[r];
+        ST(F_T2, r) = g.t2[r];
+        ST(F_C1, r) = (int32_t)g.c1[r];
     }
 #undef ST
     if (g.s0 >= 0) session_store<R>(g, p, i);
@@ -122,7 +132,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevState S, DevParams p) {
     const uint32_t gid = (uint32_t)(p.g0 + i);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) S.st[((int64_t)f * R + r) * G + i] = 0;
+        for (int f = 0; f < F_DEV; ++f) S.st[((int64_t)f * R + r) * G + i] = 0;
         S.st[((int64_t)RAFT_F_VOTED * R + r) * G + i] = -1;                 // RaftServer.kt:39
         // the timer started by init (RaftServer.kt:58, Commons.kt:14)
         const u32x4 w = draw(p, RAFT_RNG_INIT_STEP, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
@@ -138,14 +148,19 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevState S, DevParams p) {
     S.gx[G + i] = 0;
 }
 
-// K lockstep steps of every group; per-step per-block counter partials.
+// K lockstep steps of every group.  Counter partials are per wave and per
+// step, packed 16-bit pairs [k][NCW][nwaves]: no block barrier in the loop.
+#ifndef RAFT_STEP_WAVES_PER_EU
+#define RAFT_STEP_WAVES_PER_EU 1
+#endif
 template <int R>
-__global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, uint32_t t0, int nsteps,
-                                                     int32_t* __restrict__ partials) {
-    __shared__ uint32_t red[WAVES_PER_BLOCK][NCW];
+__global__ __launch_bounds__(BLOCK, RAFT_STEP_WAVES_PER_EU) void step_kernel(DevState S, DevParams p, uint32_t t0, int nsteps,
+                                                     uint32_t* __restrict__ partials) {
     const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < p.G;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * WAVES_PER_BLOCK;
+    const int wid = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
 
     Group<R> g;
     if (live) load_group<R>(g, S, p, i);
@@ -156,42 +171,47 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevState S, DevParams p, ui
         Ctx ctx{t0 + (uint32_t)k, (uint32_t)(p.g0 + i), i, -1, 0u,
                 p.log + (live ? i : 0) * (int64_t)R * p.cap, p.cap, &cnt};
         if (live) st.step(g, p, ctx);
-        // block partial of every counter for this step (no atomics: written, then reduced)
 #pragma unroll
         for (int c = 0; c < NCW; ++c) {
             const uint32_t v = __ockl_wfred_add_u32(cnt.w[c]);
-            if (lane == 0) red[wave][c] = v;
+            if (lane == 0) partials[((int64_t)k * NCW + c) * nwaves + wid] = v;
         }
-        __syncthreads();
-        if (threadIdx.x < NC) {
-            const int c = threadIdx.x;
-            uint32_t v = 0;
-#pragma unroll
-            for (int w = 0; w < WAVES_PER_BLOCK; ++w) v += (red[w][c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-            partials[((int64_t)k * NC + c) * gridDim.x + blockIdx.x] = (int32_t)v;
-        }
-        __syncthreads();
     }
     if (live) store_group<R>(g, S, p, i);
 }
 
-// counters[k][c] = sum over blocks b of partials[k][c][b]: one workgroup per
-// (step, counter), a contiguous strided sweep + wave/LDS tree.
-__global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const int32_t* __restrict__ partials, int nblocks,
+// (re)derive the log-tail cache from lastIndex and the log (after host writes)
+template <int R>
+__global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevState S, DevParams p) {
+    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= p.G) return;
+    const int64_t G = p.G;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int32_t last = S.st[((int64_t)RAFT_F_LAST * R + r) * G + i];
+        const uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
+        const uint2 a = last >= 1 ? lr[last - 1] : make_uint2(0u, 0u);
+        const uint2 b = last >= 2 ? lr[last - 2] : make_uint2(0u, 0u);
+        S.st[((int64_t)F_T1 * R + r) * G + i] = (int32_t)a.x;
+        S.st[((int64_t)F_C1 * R + r) * G + i] = (int32_t)a.y;
+        S.st[((int64_t)F_T2 * R + r) * G + i] = (int32_t)b.x;
+    }
+}
+
+// counters[k][c] = sum over waves w of the 16-bit half (c & 1) of
+// partials[k][c >> 1][w]: one workgroup per (step, counter).
+__global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* __restrict__ partials, int nwaves,
                                                                 int64_t* __restrict__ counters) {
     __shared__ int64_t acc[WAVES_PER_BLOCK];
     const int k = blockIdx.x / RAFT_COUNTER_STRIDE, c = blockIdx.x % RAFT_COUNTER_STRIDE;
-    int64_t v = 0;
+    uint32_t v = 0;                 // per-thread partial: < 2^16 * nwaves / BLOCK, fits
     if (c < NC) {
-        const int32_t* src = partials + ((int64_t)k * NC + c) * nblocks;
-        for (int b = threadIdx.x; b < nblocks; b += BLOCK) v += src[b];
+        const uint32_t* src = partials + ((int64_t)k * NCW + (c >> 1)) * nwaves;
+        const int sh = 16 * (c & 1);
+        for (int w = threadIdx.x; w < nwaves; w += BLOCK) v += (src[w] >> sh) & 0xFFFFu;
     }
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)((uint64_t)v >> 32);
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t s = ((uint64_t)hi << 32 | lo) + ((uint64_t)__shfl_xor(hi, o, 64) << 32 | __shfl_xor(lo, o, 64));
-        lo = (uint32_t)s; hi = (uint32_t)(s >> 32);
-    }
-    if ((threadIdx.x & 63) == 0) acc[threadIdx.x >> 6] = (int64_t)((uint64_t)hi << 32 | lo);
+    const uint32_t ws = __ockl_wfred_add_u32(v);   // < 2^32 for any G < 2^31 / 8 per step
+    if ((threadIdx.x & 63) == 0) acc[threadIdx.x >> 6] = ws;
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t s = 0;
@@ -289,7 +309,9 @@ __global__ __launch_bounds__(BLOCK) void digest_kernel(DevState S, DevParams p, 
 struct RepState {
     int32_t term, voted, role, commit, last, phys, elec, phase, retry;
     uint32_t fl;
-    __device__ Rep ref() { return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl}; }
+    int32_t t1, t2;
+    uint32_t c1;
+    __device__ Rep ref() { return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl, t1, t2, c1}; }
 };
 
 __device__ __forceinline__ void load_rep(RepState& x, const DevState& S, int R, int64_t G, int64_t i, int r) {
@@ -298,6 +320,14 @@ __device__ __forceinline__ void load_rep(RepState& x, const DevState& S, int R, 
     x.last = LD(RAFT_F_LAST); x.phys = LD(RAFT_F_PHYS); x.elec = LD(RAFT_F_ELECTION_MS);
     x.fl = (uint32_t)LD(RAFT_F_FLAGS); x.phase = LD(RAFT_F_PHASE_MS); x.retry = LD(RAFT_F_RETRY_MS);
 #undef LD
+}
+
+// the batch path derives the tail cache from the log (the HBM copy may be stale)
+__device__ __forceinline__ void derive_cache(RepState& x, const uint2* lr) {
+    const uint2 a = x.last >= 1 ? lr[x.last - 1] : make_uint2(0u, 0u);
+    x.t1 = (int32_t)a.x;
+    x.c1 = a.y;
+    x.t2 = x.last >= 2 ? (int32_t)lr[x.last - 2].x : 0;
 }
 
 __device__ __forceinline__ void store_rep(const RepState& x, const DevState& S, int R, int64_t G, int64_t i, int r) {
@@ -331,6 +361,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevState S, DevParams p, u
     RepState x;
     load_rep(x, S, R, p.G, i, r);
     uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
+    derive_cache(x, lr);
     Counters cnt;
     cnt.clear();
     for (int m = off[k]; m < off[k + 1]; ++m) {
@@ -343,9 +374,11 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevState S, DevParams p, u
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
             int32_t rt = 0; bool su = false;
-            const bool okh = append_handler(x.ref(), r + 1, lr, p.cap, q.term, q.leader_id, q.prev_log_index,
+            const int32_t pv = q.prev_log_index;
+            const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lr[pv].x : 0;
+            const bool okh = append_handler(x.ref(), r + 1, lr, p.cap, q.term, q.leader_id, pv,
                                             q.prev_log_term, q.has_entry != 0, Entry{q.entry_term, q.entry_cmd},
-                                            q.leader_commit, cnt, rt, su);
+                                            q.leader_commit, dprev, cnt, rt, su);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, su ? 1 : 0, okh ? 0 : 1};
         } else {
             append_command(x.ref(), lr, p.cap, ((const uint32_t*)req)[o], cnt);
@@ -371,9 +404,10 @@ struct raft_engine {
     uint64_t t;
     int K;                      // steps per launch
     int nblocks;
-    int32_t* partials;          // [K][nblocks][NC]
+    uint32_t* partials;         // [K][NCW][nwaves] packed per-wave counter partials
     int64_t* counters_dev;      // [K][STRIDE] scratch
     // step-kernel event timing
+    bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
     bool timing;
     std::vector<hipEvent_t> ev;  // pool, pairs
     size_t ev_used;
@@ -399,6 +433,11 @@ template <int R> struct InitL {
     static void run(raft_engine* e) {
         const unsigned nb = (unsigned)((e->p.G + BLOCK - 1) / BLOCK);
         init_kernel<R><<<nb, BLOCK, 0, e->stream>>>(e->S, e->dp);
+    }
+};
+template <int R> struct RebuildL {
+    static void run(raft_engine* e) {
+        rebuild_cache_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->S, e->dp);
     }
 };
 template <int R> struct StepL {
@@ -473,6 +512,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     raft_engine* e = new raft_engine();
     e->p = *p;
     e->timing = false;
+    e->cache_valid = true;
     e->ev_used = 0;
     e->timed_launches = 0;
     e->device = device;
@@ -490,12 +530,12 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->nblocks = (int)((G + BLOCK - 1) / BLOCK);
     e->K = p->steps_per_launch > 0 ? p->steps_per_launch : 1;
 
-    const size_t st_b = (size_t)RAFT_NUM_FIELDS * R * G * 4;
+    const size_t st_b = (size_t)F_DEV * R * G * 4;
     const size_t ses_b = (size_t)R * R * G * 4;
     const size_t gx_b = (size_t)2 * G * 4;
     const size_t log_b = (size_t)G * R * p->log_cap * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t part_b = (size_t)e->K * e->nblocks * NC * 4;
+    const size_t part_b = (size_t)e->K * NCW * e->nblocks * WAVES_PER_BLOCK * 4;
     const size_t cnt_b = (size_t)e->K * RAFT_COUNTER_STRIDE * 8;
     e->bytes = al(st_b) + 2 * al(ses_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -511,7 +551,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->S.nx = (int32_t*)b; b += al(ses_b);
     e->S.mt = (int32_t*)b; b += al(ses_b);
     e->S.gx = (int32_t*)b; b += al(gx_b);
-    e->partials = (int32_t*)b; b += al(part_b);
+    e->partials = (uint32_t*)b; b += al(part_b);
     e->counters_dev = (int64_t*)b; b += al(cnt_b);
     e->S.log = (uint2*)b;
     d.log = e->S.log;
@@ -544,6 +584,10 @@ int raft_engine_destroy(raft_engine* e) {
 int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_dev) {
     if (!e || n_steps < 0) return fail(RAFT_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(e->device));
+    if (!e->cache_valid && n_steps > 0) {
+        dispatch_R<RebuildL>(e->p.R, e);
+        e->cache_valid = true;
+    }
     for (int32_t done = 0; done < n_steps;) {
         const int k = std::min<int32_t>(e->K, n_steps - done);
         if (e->timing) {
@@ -562,7 +606,7 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
             e->ev_used += 2;
         }
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
-        reduce_counters_kernel<<<k * RAFT_COUNTER_STRIDE, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, dst);
+        reduce_counters_kernel<<<k * RAFT_COUNTER_STRIDE, BLOCK, 0, e->stream>>>(e->partials, e->nblocks * WAVES_PER_BLOCK, dst);
         done += k;
     }
     HIP_TRY(hipGetLastError());
@@ -661,6 +705,7 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
     int32_t* buf = nullptr;
     HIP_TRY(hipMalloc(&buf, bytes));
     hipError_t err = hipMemcpyAsync(buf, in, bytes, hipMemcpyHostToDevice, e->stream);
+    e->cache_valid = false;
     if (err == hipSuccess) {
         dispatch_R<UnpackL>(e->p.R, e, g0, n, buf);
         err = hipStreamSynchronize(e->stream);
@@ -692,6 +737,7 @@ int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* 
     const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
     std::vector<uint2> tmp(cnt);
     for (size_t k = 0; k < cnt; ++k) tmp[k] = make_uint2((uint32_t)terms[k], cmds[k]);
+    e->cache_valid = false;
     HIP_TRY(hipMemcpyAsync(e->S.log + (size_t)g0 * e->p.R * e->p.log_cap, tmp.data(), cnt * 8,
                            hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -737,6 +783,7 @@ static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32
     off.push_back(n);
     const int nk = (int)keys.size();
     HIP_TRY(hipSetDevice(e->device));
+    e->cache_valid = false;
     const size_t b_keys = nk * 8, b_off = (nk + 1) * 8, b_ord = n * 8, b_req = n * req_sz, b_resp = n * resp_sz;
     char* buf = nullptr;
     HIP_TRY(hipMalloc(&buf, b_keys + b_off + b_ord + b_req + b_resp + 64));

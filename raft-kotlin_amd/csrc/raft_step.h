@@ -87,12 +87,21 @@ struct Ctx {
 struct Rep {
     int32_t &term, &voted, &role, &commit, &last, &phys, &elec, &phase, &retry;
     uint32_t& fl;
+    int32_t &t1, &t2;          // log-tail cache: term of log[last-1], log[last-2]
+    uint32_t& c1;              //                 cmd  of log[last-1]
 };
 
 // Pick / replace element s of a register array for a per-lane runtime s,
 // given as the one-hot mask 1 << s.  Written as masked OR / blend so the
 // optimiser cannot turn it into a dynamically indexed load or store (which
 // would demote the whole register array to scratch memory).
+template <int R>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[R], uint32_t onehot) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v |= a[r] & (0u - ((onehot >> r) & 1u));
+    return v;
+}
 template <int R>
 __device__ __forceinline__ int32_t pick(const int32_t (&a)[R], uint32_t onehot) {
     int32_t v = 0;
@@ -120,19 +129,38 @@ __device__ __forceinline__ void send_follower(Rep n) {
 }
 
 // ---- Log<T> (Commons.kt:47-74) over one replica's HBM slots ---------------
+// The engine keeps a 2-deep tail cache per replica (t1 = log[last-1].term,
+// t2 = log[last-2].term, c1 = log[last-1].cmd; derived state, never
+// exported).  In steady state every read the handlers make (prev checks,
+// the newest entry, vote last-terms) hits it; HBM is read only for older
+// slots and when the ghost tail resurfaces a stale slot.
+__device__ __forceinline__ int32_t term_at(const uint2* lr, int32_t last, int32_t t1, int32_t t2, int32_t j) {
+    return j == last - 1 ? t1 : j == last - 2 ? t2 : (int32_t)lr[j].x;
+}
+
 // Log.add(i, e): 1 true, 0 false, -1 capacity overflow (counted), -2 threw
-__device__ __forceinline__ int log_add(uint2* lr, int cap, int32_t& last, int32_t& phys, int32_t i, Entry e) {
-    if (last == i) {                                   // :58-61 append at the PHYSICAL end (Q1)
-        if (phys >= cap) return -1;
-        lr[phys] = make_uint2((uint32_t)e.term, e.cmd);
-        phys += 1;
-        last += 1;
+__device__ __forceinline__ int log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e) {
+    if (n.last == i) {                                 // :58-61 append at the PHYSICAL end (Q1)
+        if (n.phys >= cap) return -1;
+        lr[n.phys] = make_uint2((uint32_t)e.term, e.cmd);
+        if (n.phys == n.last) {                        // no ghost: the new last entry is e
+            n.t2 = n.t1; n.t1 = e.term; n.c1 = e.cmd;
+        } else {                                       // ghost: stale slot log[last] resurfaces
+            const uint2 gs = lr[n.last];
+            n.t2 = n.t1; n.t1 = (int32_t)gs.x; n.c1 = gs.y;
+        }
+        n.phys += 1;
+        n.last += 1;
         return 1;
     }
-    if (last < i) return 0;                            // :62
+    if (n.last < i) return 0;                          // :62
     if (i < 0) return -2;
     lr[i] = make_uint2((uint32_t)e.term, e.cmd);       // :63-66 overwrite, no shrink
-    last = i + 1;
+    // new last = i + 1; log[i-1] is unchanged
+    n.t2 = i == 0 ? 0 : (i == n.last - 1 ? n.t2 : (int32_t)lr[i - 1].x);
+    n.t1 = e.term;
+    n.c1 = e.cmd;
+    n.last = i + 1;
     return 1;
 }
 
@@ -145,7 +173,7 @@ __device__ __forceinline__ void vote_handler(Rep n, const uint2* lr, int32_t rt,
         granted = n.voted == rc;
     } else {
         int32_t lt = 0;
-        if (n.last >= 1) { lt = (int32_t)lr[n.last - 1].x; cnt.add(RAFT_C_VOTE_LOG_READS); }
+        if (n.last >= 1) { lt = n.t1; cnt.add(RAFT_C_VOTE_LOG_READS); }
         if (n.last >= 1 && rlt < lt) {
         } else if (n.last >= 1 && rlt == lt && rli < n.last) {
         } else {
@@ -159,9 +187,12 @@ __device__ __forceinline__ void vote_handler(Rep n, const uint2* lr, int32_t rt,
 }
 
 // ---- append() (RaftServer.kt:253-287); returns false where it throws -------
+// dprev = term of this replica's log[prev], read by the caller ahead of time
+// (valid whenever 0 <= prev < lastIndex, the only case it is used).
 __device__ __forceinline__ bool append_handler(Rep n, int32_t id, uint2* lr, int cap, int32_t rt, int32_t rlead,
                                                int32_t prev, int32_t prevTerm, bool has, Entry e,
-                                               int32_t lcommit, Counters& cnt, int32_t& resp_term, bool& success) {
+                                               int32_t lcommit, int32_t dprev, Counters& cnt, int32_t& resp_term,
+                                               bool& success) {
     if (rt > n.term) {                                  // :257-262
         n.term = rt; n.voted = -1; n.role = RAFT_FOLLOWER;
         send_follower(n);
@@ -179,10 +210,10 @@ __device__ __forceinline__ bool append_handler(Rep n, int32_t id, uint2* lr, int
     else if (n.last > prev) {
         if (prev < 0) { resp_term = n.term; success = false; return false; }
         cnt.add(RAFT_C_PREV_READS_FOLLOWER);
-        success = (int32_t)lr[prev].x == prevTerm;
+        success = dprev == prevTerm;
     } else success = false;
     if (success && has) {                               // :278 (Q2, Q10)
-        const int r = log_add(lr, cap, n.last, n.phys, prev + 1, e);
+        const int r = log_add(lr, cap, n, prev + 1, e);
         if (r == 1) cnt.add(RAFT_C_ENTRY_WRITES);
         else if (r == -1) cnt.add(RAFT_C_LOG_OVERFLOW);
     }
@@ -192,7 +223,7 @@ __device__ __forceinline__ bool append_handler(Rep n, int32_t id, uint2* lr, int
 
 // ---- appendCommand() (RaftServer.kt:100-107) ------------------------------
 __device__ __forceinline__ void append_command(Rep n, uint2* lr, int cap, uint32_t cmd, Counters& cnt) {
-    const int r = log_add(lr, cap, n.last, n.phys, n.last, Entry{n.term, cmd});
+    const int r = log_add(lr, cap, n, n.last, Entry{n.term, (uint32_t)cmd});
     cnt.add(RAFT_C_COMMANDS);
     if (r == -1) cnt.add(RAFT_C_LOG_OVERFLOW);
 }
@@ -204,12 +235,15 @@ template <int R>
 struct Group {
     int32_t term[R], voted[R], role[R], commit[R], last[R], phys[R], elec[R], phase[R], retry[R];
     uint32_t fl[R];
+    int32_t t1[R], t2[R];           // log-tail cache (terms of log[last-1], log[last-2])
+    uint32_t c1[R];                 //                (cmd of log[last-1])
     int32_t s0;                     // owner of the primary session in registers, -1 none
     int32_t nx0[R], mc0[R];         // its nextIndex / matchIndex (RaftServer.kt:112-113)
     int32_t iso, cmdc;              // harness: isolation word, commands issued
 
     __device__ __forceinline__ Rep rep(int r) {
-        return Rep{term[r], voted[r], role[r], commit[r], last[r], phys[r], elec[r], phase[r], retry[r], fl[r]};
+        return Rep{term[r], voted[r], role[r], commit[r], last[r], phys[r], elec[r], phase[r], retry[r], fl[r],
+                   t1[r], t2[r], c1[r]};
     }
 };
 
@@ -271,8 +305,7 @@ struct Stepper {
         qli[r] = g.last[r];
         if (g.last[r] == 0) qlt[r] = 0;
         else {
-            const uint2* lr = c.lg + r * c.cap;
-            qlt[r] = (int32_t)lr[g.last[r] - 1].x;
+            qlt[r] = g.t1[r];                                  // log.get(lastIndex - 1).term
             c.cnt->add(RAFT_C_VOTE_LOG_READS);
         }
     }
@@ -335,29 +368,39 @@ struct Stepper {
             session_load<R>(g, p, c.i, s);
         }
         const int32_t Lterm = pick(g.term, oh), Lcommit = pick(g.commit, oh), Llast = pick(g.last, oh);
+        const int32_t Lt1 = pick(g.t1, oh), Lt2 = pick(g.t2, oh), Lc1 = (int32_t)pick(g.c1, oh);
         const uint2* ls = c.lg + s * c.cap;
-        // build every request first (RaftServer.kt:122-132)
+        // Every log slot this tick reads is resolved up front: the leader's
+        // log[prev] and log[i-1] for each request (built before any handler
+        // runs, RaftServer.kt:122-132) and each follower's own log[prev]
+        // (append() :274-276).  The tail cache answers the steady-state ones;
+        // the rest are loaded in one batch.  A handler only writes its own
+        // replica's log, so no earlier handler of the tick can change a slot a
+        // later one reads.
+        int32_t lpt[R], dpt[R];
+        uint2 lent[R];
+#pragma unroll
+        for (int d = 0; d < R; ++d) {
+            const int32_t i = g.nx0[d], prev = i - 2;
+            lpt[d] = (prev >= 0 && prev <= Llast - 1) ? term_at(ls, Llast, Lt1, Lt2, prev) : -1;
+            lent[d] = (i >= 1 && i <= Llast) ? (i == Llast ? make_uint2((uint32_t)Lt1, (uint32_t)Lc1) : ls[i - 1])
+                                             : make_uint2(0u, 0u);
+            const uint2* lr = c.lg + d * c.cap;
+            dpt[d] = (prev >= 0 && prev < g.last[d]) ? term_at(lr, g.last[d], g.t1[d], g.t2[d], prev) : 0;
+        }
+        // build every request (RaftServer.kt:122-132)
         uint32_t okm = 0, hasm = 0;
-        int32_t pvt[R];
-        Entry ent[R];
 #pragma unroll
         for (int d = 0; d < R; ++d) {
             const int32_t i = g.nx0[d], prev = i - 2;
             bool ok = true;
-            pvt[d] = -1;
-            ent[d] = Entry{0, 0u};
             if (prev >= 0) {                                           // :128 (Q11)
                 if (prev > Llast - 1) ok = false;
-                else { pvt[d] = (int32_t)ls[prev].x; cnt.add(RAFT_C_PREV_READS_LEADER); }
+                else cnt.add(RAFT_C_PREV_READS_LEADER);
             }
             if (ok && Llast >= i) {                                    // :130-131
                 if (i - 1 < 0) ok = false;
-                else {
-                    const uint2 e = ls[i - 1];
-                    ent[d] = Entry{(int32_t)e.x, e.y};
-                    hasm |= 1u << d;
-                    cnt.add(RAFT_C_ENTRY_READS_LEADER);
-                }
+                else { hasm |= 1u << d; cnt.add(RAFT_C_ENTRY_READS_LEADER); }
             }
             if (ok) okm |= 1u << d;
             else cnt.add(RAFT_C_APPEND_SKIPPED);
@@ -374,8 +417,8 @@ struct Stepper {
             const int32_t prev = g.nx0[d] - 2;
             const bool has = (hasm >> d) & 1u;
             int32_t rterm; bool succ;
-            if (!append_handler(g.rep(d), d + 1, c.lg + d * c.cap, c.cap, Lterm, s + 1, prev, pvt[d], has, ent[d],
-                                Lcommit, cnt, rterm, succ))
+            if (!append_handler(g.rep(d), d + 1, c.lg + d * c.cap, c.cap, Lterm, s + 1, prev, lpt[d], has,
+                                Entry{(int32_t)lent[d].x, lent[d].y}, Lcommit, dpt[d], cnt, rterm, succ))
                 continue;
             if (lost(p, c, du, s, d, 1)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
             if (rterm > T) { T = rterm; stepdown = true; continue; }  // :146-154 (Q7)
