@@ -1,17 +1,11 @@
 // raft_engine.hip — HIP kernels (gfx950) and the C-ABI of include/raft_engine.h.
 //
-// HBM layout (structure of arrays, lane = group, so every state access of a
-// wave is one contiguous 256-byte run per field):
-//   st  int32 [F_DEV][R][G]               per-replica scalars (RaftServer.kt:35-48): the
-//                                         RAFT_NUM_FIELDS canonical ones, then the
-//                                         engine-internal log-tail cache (t1, t2, c1)
-//   nx  int32 [R][R][G]                   nextIndex  of replica s's session towards d
-//   mt  int32 [R][R][G]                   matchIndex (RaftServer.kt:112-113)
-//   gx  int32 [2][G]                      harness words (isolation, commands issued)
-//   log uint2 [G][R][log_cap]             (term, cmd) physical log slots (Commons.kt:51)
-// The step kernel keeps a group in VGPRs for the whole launch (1..K fused
-// lockstep steps) and touches HBM only for the state load/store at the launch
-// edges and the log slots the handlers read or write.
+// HBM layout: see raft_step.h (DevParams).  Per-replica arrays are indexed by
+// g * R + r, so one wave (GPW = 64 / R whole groups, one lane per replica)
+// reads or writes one contiguous run per field.  The step kernel keeps every
+// replica in VGPRs for a whole launch (1..K fused lockstep steps) and touches
+// HBM only for the state load/store at the launch edges, the log slots the
+// handlers read or write, and (rarely) non-primary session rows.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -40,162 +34,175 @@ int fail(int code, const std::string& msg) {
             return fail(RAFT_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
 
-struct DevState {
-    int32_t* st;
-    int32_t* nx;
-    int32_t* mt;
-    int32_t* gx;
-    uint2* log;
-};
-
-constexpr int F_T1 = RAFT_NUM_FIELDS, F_T2 = RAFT_NUM_FIELDS + 1, F_C1 = RAFT_NUM_FIELDS + 2;
-constexpr int F_DEV = RAFT_NUM_FIELDS + 3;
 constexpr int BLOCK = 256;
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
 
 // ---------------------------------------------------------------------------
-// state <-> registers
+// replica state <-> registers
 // ---------------------------------------------------------------------------
-template <int R>
-__device__ __forceinline__ void load_group(Group<R>& g, const DevState& S, const DevParams& p, int64_t i) {
-    const int64_t G = p.G;
-#define LD(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        g.term[r] = LD(RAFT_F_TERM, r);
-        g.voted[r] = LD(RAFT_F_VOTED, r);
-        g.role[r] = LD(RAFT_F_ROLE, r);
-        g.commit[r] = LD(RAFT_F_COMMIT, r);
-        g.last[r] = LD(RAFT_F_LAST, r);
-        g.phys[r] = LD(RAFT_F_PHYS, r);
-        g.elec[r] = LD(RAFT_F_ELECTION_MS, r);
-        g.fl[r] = (uint32_t)LD(RAFT_F_FLAGS, r);
-        g.phase[r] = LD(RAFT_F_PHASE_MS, r);
-        g.retry[r] = LD(RAFT_F_RETRY_MS, r);
-        g.t1[r] = LD(F_T1, r);
-        g.t2[r] = LD(F_T2, r);
-        g.c1[r] = (uint32_t)LD(F_C1, r);
-    }
-#undef LD
-    // the lowest active leader session becomes the register-resident primary
-    int s0 = -1;
-#pragma unroll
-    for (int r = R - 1; r >= 0; --r) if (g.fl[r] & FL_HB) s0 = r;
-    g.s0 = -1;
-#pragma unroll
-    for (int d = 0; d < R; ++d) { g.nx0[d] = 0; g.mc0[d] = 0; }
-    if (s0 >= 0) session_load<R>(g, p, i, s0);
-    g.iso = S.gx[i];
-    g.cmdc = S.gx[G + i];
+__device__ __forceinline__ void load_node(Node& n, const DevParams& p, int64_t g, int64_t idx) {
+    const int32_t* st = p.st;
+    n.term = st[fidx(p, RAFT_F_TERM, idx)];
+    n.voted = st[fidx(p, RAFT_F_VOTED, idx)];
+    n.role = st[fidx(p, RAFT_F_ROLE, idx)];
+    n.commit = st[fidx(p, RAFT_F_COMMIT, idx)];
+    n.last = st[fidx(p, RAFT_F_LAST, idx)];
+    n.phys = st[fidx(p, RAFT_F_PHYS, idx)];
+    n.elec = st[fidx(p, RAFT_F_ELECTION_MS, idx)];
+    n.fl = (uint32_t)st[fidx(p, RAFT_F_FLAGS, idx)];
+    n.phase = st[fidx(p, RAFT_F_PHASE_MS, idx)];
+    n.retry = st[fidx(p, RAFT_F_RETRY_MS, idx)];
+    n.t1 = st[fidx(p, F_T1, idx)];
+    n.t2 = st[fidx(p, F_T2, idx)];
+    n.c1 = (uint32_t)st[fidx(p, F_C1, idx)];
+    n.nx = p.ses[idx];
+    n.mc = p.ses[p.GR + idx];
+    n.iso = p.gx[GX_ISO * p.G + g];
+    n.cmdc = p.gx[GX_CMDS * p.G + g];
+    n.s0 = p.gx[GX_S0 * p.G + g];
 }
 
-template <int R>
-__device__ __forceinline__ void store_group(const Group<R>& g, const DevState& S, const DevParams& p, int64_t i) {
-    const int64_t G = p.G;
-#define ST(f, r) S.st[((int64_t)(f) * R + (r)) * G + i]
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        ST(RAFT_F_TERM, r) = g.term[r];
-        ST(RAFT_F_VOTED, r) = g.voted[r];
-        ST(RAFT_F_ROLE, r) = g.role[r];
-        ST(RAFT_F_COMMIT, r) = g.commit[r];
-        ST(RAFT_F_LAST, r) = g.last[r];
-        ST(RAFT_F_PHYS, r) = g.phys[r];
-        ST(RAFT_F_ELECTION_MS, r) = g.elec[r];
-        ST(RAFT_F_FLAGS, r) = (int32_t)(g.fl[r] & FL_EXPORT_MASK);
-        ST(RAFT_F_PHASE_MS, r) = g.phase[r];
-        ST(RAFT_F_RETRY_MS, r) = g.retry[r];
-        ST(F_T1, r) = g.t1[r];
-        ST(F_T2, r) = g.t2[r];
-        ST(F_C1, r) = (int32_t)g.c1[r];
+__device__ __forceinline__ void inert_node(Node& n) {
+    n.term = n.commit = n.last = n.phys = n.elec = n.phase = n.retry = 0;
+    n.voted = -1;
+    n.role = RAFT_FOLLOWER;
+    n.fl = 0;
+    n.t1 = n.t2 = 0;
+    n.c1 = 0;
+    n.nx = n.mc = 0;
+    n.iso = n.cmdc = 0;
+    n.s0 = -1;
+}
+
+__device__ __forceinline__ void store_node(const Node& n, const DevParams& p, int64_t g, int64_t idx, bool group_lead) {
+    int32_t* st = p.st;
+    st[fidx(p, RAFT_F_TERM, idx)] = n.term;
+    st[fidx(p, RAFT_F_VOTED, idx)] = n.voted;
+    st[fidx(p, RAFT_F_ROLE, idx)] = n.role;
+    st[fidx(p, RAFT_F_COMMIT, idx)] = n.commit;
+    st[fidx(p, RAFT_F_LAST, idx)] = n.last;
+    st[fidx(p, RAFT_F_PHYS, idx)] = n.phys;
+    st[fidx(p, RAFT_F_ELECTION_MS, idx)] = n.elec;
+    st[fidx(p, RAFT_F_FLAGS, idx)] = (int32_t)(n.fl & FL_EXPORT_MASK);
+    st[fidx(p, RAFT_F_PHASE_MS, idx)] = n.phase;
+    st[fidx(p, RAFT_F_RETRY_MS, idx)] = n.retry;
+    st[fidx(p, F_T1, idx)] = n.t1;
+    st[fidx(p, F_T2, idx)] = n.t2;
+    st[fidx(p, F_C1, idx)] = (int32_t)n.c1;
+    p.ses[idx] = n.nx;
+    p.ses[p.GR + idx] = n.mc;
+    if (group_lead) {
+        p.gx[GX_ISO * p.G + g] = n.iso;
+        p.gx[GX_CMDS * p.G + g] = n.cmdc;
+        p.gx[GX_S0 * p.G + g] = n.s0;
     }
-#undef ST
-    if (g.s0 >= 0) session_store<R>(g, p, i);
-    S.gx[i] = g.iso;
-    S.gx[G + i] = g.cmdc;
+}
+
+// canonical session rows: the primary (owner s0) lives in ses, the rest in spill
+__device__ __forceinline__ int32_t canon_next(const DevParams& p, int R, int64_t g, int s0, int s, int d) {
+    const int64_t idx = g * R + d;
+    return s == s0 ? p.ses[idx] : p.spill[idx * R + s];
+}
+__device__ __forceinline__ int32_t canon_match(const DevParams& p, int R, int64_t g, int s0, int s, int d) {
+    const int64_t idx = g * R + d;
+    return s == s0 ? p.ses[p.GR + idx] : p.spill[p.GR * R + idx * R + s];
 }
 
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
+// one thread per replica: the reference's initial node (RaftServer.kt:35-48)
+// with the election timer started by init (RaftServer.kt:58, Commons.kt:14)
 template <int R>
-__global__ __launch_bounds__(BLOCK) void init_kernel(DevState S, DevParams p) {
-    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= p.G) return;
-    const int64_t G = p.G;
-    const uint32_t gid = (uint32_t)(p.g0 + i);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        for (int f = 0; f < F_DEV; ++f) S.st[((int64_t)f * R + r) * G + i] = 0;
-        S.st[((int64_t)RAFT_F_VOTED * R + r) * G + i] = -1;                 // RaftServer.kt:39
-        // the timer started by init (RaftServer.kt:58, Commons.kt:14)
-        const u32x4 w = draw(p, RAFT_RNG_INIT_STEP, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
-        S.st[((int64_t)RAFT_F_ELECTION_MS * R + r) * G + i] = scale_range(word_of(w, r & 3), p.emin, p.emax);
-        S.st[((int64_t)RAFT_F_FLAGS * R + r) * G + i] = (int32_t)FL_ARMED;
-#pragma unroll
-        for (int d = 0; d < R; ++d) {
-            S.nx[((int64_t)r * R + d) * G + i] = 0;
-            S.mt[((int64_t)r * R + d) * G + i] = 0;
-        }
+__global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
+    const int64_t idx = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (idx >= p.GR) return;
+    const int64_t g = idx / R;
+    const int r = (int)(idx - g * R);
+    const uint32_t gid = (uint32_t)(p.g0 + g);
+    for (int f = 0; f < F_DEV; ++f) p.st[fidx(p, f, idx)] = 0;
+    p.st[fidx(p, RAFT_F_VOTED, idx)] = -1;                               // RaftServer.kt:39
+    const u32x4 w = draw(p, RAFT_RNG_INIT_STEP, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
+    p.st[fidx(p, RAFT_F_ELECTION_MS, idx)] = scale_range(word_of(w, r & 3), p.emin, p.emax);
+    p.st[fidx(p, RAFT_F_FLAGS, idx)] = (int32_t)FL_ARMED;
+    p.ses[idx] = 0;
+    p.ses[p.GR + idx] = 0;
+    for (int s = 0; s < R; ++s) {
+        p.spill[idx * R + s] = 0;
+        p.spill[p.GR * R + idx * R + s] = 0;
     }
-    S.gx[i] = 0;
-    S.gx[G + i] = 0;
+    if (r == 0) {
+        p.gx[GX_ISO * p.G + g] = 0;
+        p.gx[GX_CMDS * p.G + g] = 0;
+        p.gx[GX_S0 * p.G + g] = -1;
+    }
 }
 
-// K lockstep steps of every group.  Counter partials are per wave and per
-// step, packed 16-bit pairs [k][NCW][nwaves]: no block barrier in the loop.
-#ifndef RAFT_STEP_WAVES_PER_EU
-#define RAFT_STEP_WAVES_PER_EU 1
-#endif
+// K lockstep steps of every group.  A wave holds GPW whole groups, one lane
+// per replica.  Counter partials are per wave and per step, packed 16-bit
+// pairs [k][NCW][nwaves]: no block barrier anywhere in the kernel.
 template <int R>
-__global__ __launch_bounds__(BLOCK, RAFT_STEP_WAVES_PER_EU) void step_kernel(DevState S, DevParams p, uint32_t t0, int nsteps,
+__global__ __launch_bounds__(BLOCK) void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
-    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const bool live = i < p.G;
+    using L = Lanes<R>;
     const int lane = threadIdx.x & 63;
-    const int nwaves = gridDim.x * WAVES_PER_BLOCK;
     const int wid = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int nwaves = gridDim.x * WAVES_PER_BLOCK;
+    const int j = lane / R;
+    const int r = lane - j * R;
+    const int64_t g = (int64_t)wid * L::GPW + j;
+    const bool live = j < L::GPW && g < p.G;
 
-    Group<R> g;
-    if (live) load_group<R>(g, S, p, i);
-    Stepper<R> st;
+    Ctx<R> c;
+    c.r = r;
+    c.base = j * R;
+    c.live = live;
+    c.idx = g * R + r;
+    c.gid = (uint32_t)(p.g0 + g);
+    c.lr = p.log + (live ? c.idx : 0) * (int64_t)p.cap;
+    c.iso = -1;
+    c.part = 0;
+    c.job = u32x4{0u, 0u, 0u, 0u};
+
+    Node n;
+    if (live) load_node(n, p, g, c.idx);
+    else inert_node(n);
     for (int k = 0; k < nsteps; ++k) {
+        const uint32_t t = t0 + (uint32_t)k;
+        c.t = t;
+        if (p.part_period > 0) {                                          // S-11 partitions
+            const uint32_t ph = t % (uint32_t)p.part_period;
+            if ((int64_t)ph < p.part_len) {
+                if (k == 0 || ph == 0) c.part = draw(p, t - ph, c.gid, RAFT_RNG_PARTITION, 0).x & L::ALL;
+            } else {
+                c.part = 0;
+            }
+        }
         Counters cnt;
         cnt.clear();
-        Ctx ctx{t0 + (uint32_t)k, (uint32_t)(p.g0 + i), i, -1, 0u,
-                p.log + (live ? i : 0) * (int64_t)R * p.cap, p.cap, &cnt};
-        if (live) st.step(g, p, ctx);
+        Stepper<R>::step(p, c, n, cnt);
 #pragma unroll
-        for (int c = 0; c < NCW; ++c) {
-            const uint32_t v = __ockl_wfred_add_u32(cnt.w[c]);
-            if (lane == 0) partials[((int64_t)k * NCW + c) * nwaves + wid] = v;
+        for (int cw = 0; cw < NCW; ++cw) {
+            const uint32_t v = __ockl_wfred_add_u32(cnt.w[cw]);
+            if (lane == 0) partials[((int64_t)k * NCW + cw) * nwaves + wid] = v;
         }
     }
-    if (live) store_group<R>(g, S, p, i);
+    if (live) store_node(n, p, g, c.idx, r == 0);
 }
 
 // (re)derive the log-tail cache from lastIndex and the log (after host writes)
-template <int R>
-__global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevState S, DevParams p) {
-    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= p.G) return;
-    const int64_t G = p.G;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int32_t last = S.st[((int64_t)RAFT_F_LAST * R + r) * G + i];
-        const uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
-        const uint2 a = last >= 1 ? lr[last - 1] : make_uint2(0u, 0u);
-        const uint2 b = last >= 2 ? lr[last - 2] : make_uint2(0u, 0u);
-        S.st[((int64_t)F_T1 * R + r) * G + i] = (int32_t)a.x;
-        S.st[((int64_t)F_C1 * R + r) * G + i] = (int32_t)a.y;
-        S.st[((int64_t)F_T2 * R + r) * G + i] = (int32_t)b.x;
-    }
+__global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
+    const int64_t idx = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (idx >= p.GR) return;
+    const int32_t last = p.st[fidx(p, RAFT_F_LAST, idx)];
+    const uint2* lr = p.log + idx * (int64_t)p.cap;
+    const uint2 a = last >= 1 ? lr[last - 1] : make_uint2(0u, 0u);
+    const uint2 b = last >= 2 ? lr[last - 2] : make_uint2(0u, 0u);
+    p.st[fidx(p, F_T1, idx)] = (int32_t)a.x;
+    p.st[fidx(p, F_C1, idx)] = (int32_t)a.y;
+    p.st[fidx(p, F_T2, idx)] = (int32_t)b.x;
 }
 
 // counters[k][c] = sum over waves w of the 16-bit half (c & 1) of
@@ -220,41 +227,48 @@ __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* 
     }
 }
 
-// canonical export [n][W] of groups [g0, g0+n)
+// canonical export [n][W] of groups [g0, g0+n): one thread per group
 template <int R>
-__global__ __launch_bounds__(BLOCK) void pack_kernel(DevState S, int64_t G, int64_t g0, int64_t n, int32_t* out) {
-    const int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= n) return;
-    const int64_t i = g0 + j;
+__global__ __launch_bounds__(BLOCK) void pack_kernel(DevParams p, int64_t g0, int64_t n, int32_t* out) {
+    const int64_t jx = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (jx >= n) return;
+    const int64_t g = g0 + jx;
     constexpr int W = R * RAFT_NUM_FIELDS + 2 * R * R + RAFT_GROUP_EXTRA;
-    int32_t* w = out + j * W;
+    int32_t* w = out + jx * W;
     for (int r = 0; r < R; ++r)
-        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) w[r * RAFT_NUM_FIELDS + f] = S.st[((int64_t)f * R + r) * G + i];
+        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) {
+            const int32_t v = p.st[fidx(p, f, g * R + r)];
+            w[r * RAFT_NUM_FIELDS + f] = f == RAFT_F_FLAGS ? (int32_t)((uint32_t)v & FL_EXPORT_MASK) : v;
+        }
+    const int s0 = p.gx[GX_S0 * p.G + g];
     for (int s = 0; s < R; ++s)
         for (int d = 0; d < R; ++d) {
-            w[R * RAFT_NUM_FIELDS + s * R + d] = S.nx[((int64_t)s * R + d) * G + i];
-            w[R * RAFT_NUM_FIELDS + R * R + s * R + d] = S.mt[((int64_t)s * R + d) * G + i];
+            w[R * RAFT_NUM_FIELDS + s * R + d] = canon_next(p, R, g, s0, s, d);
+            w[R * RAFT_NUM_FIELDS + R * R + s * R + d] = canon_match(p, R, g, s0, s, d);
         }
-    w[W - 2] = S.gx[i];
-    w[W - 1] = S.gx[G + i];
+    w[W - 2] = p.gx[GX_ISO * p.G + g];
+    w[W - 1] = p.gx[GX_CMDS * p.G + g];
 }
 
 template <int R>
-__global__ __launch_bounds__(BLOCK) void unpack_kernel(DevState S, int64_t G, int64_t g0, int64_t n, const int32_t* in) {
-    const int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= n) return;
-    const int64_t i = g0 + j;
+__global__ __launch_bounds__(BLOCK) void unpack_kernel(DevParams p, int64_t g0, int64_t n, const int32_t* in) {
+    const int64_t jx = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (jx >= n) return;
+    const int64_t g = g0 + jx;
     constexpr int W = R * RAFT_NUM_FIELDS + 2 * R * R + RAFT_GROUP_EXTRA;
-    const int32_t* w = in + j * W;
+    const int32_t* w = in + jx * W;
     for (int r = 0; r < R; ++r)
-        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) S.st[((int64_t)f * R + r) * G + i] = w[r * RAFT_NUM_FIELDS + f];
+        for (int f = 0; f < RAFT_NUM_FIELDS; ++f) p.st[fidx(p, f, g * R + r)] = w[r * RAFT_NUM_FIELDS + f];
+    // every session row goes to spill; no primary until a session ticks
     for (int s = 0; s < R; ++s)
         for (int d = 0; d < R; ++d) {
-            S.nx[((int64_t)s * R + d) * G + i] = w[R * RAFT_NUM_FIELDS + s * R + d];
-            S.mt[((int64_t)s * R + d) * G + i] = w[R * RAFT_NUM_FIELDS + R * R + s * R + d];
+            const int64_t idx = g * R + d;
+            p.spill[idx * R + s] = w[R * RAFT_NUM_FIELDS + s * R + d];
+            p.spill[p.GR * R + idx * R + s] = w[R * RAFT_NUM_FIELDS + R * R + s * R + d];
         }
-    S.gx[i] = w[W - 2];
-    S.gx[G + i] = w[W - 1];
+    p.gx[GX_ISO * p.G + g] = w[W - 2];
+    p.gx[GX_CMDS * p.G + g] = w[W - 1];
+    p.gx[GX_S0 * p.G + g] = -1;
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
@@ -264,26 +278,30 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     return k;
 }
 
-// order-independent state digest (DESIGN.md §3.10): sum of per-group FNV-1a/fmix64
+// order-independent state digest (DESIGN.md §3 S-13): sum of per-group FNV-1a/fmix64
 template <int R>
-__global__ __launch_bounds__(BLOCK) void digest_kernel(DevState S, DevParams p, unsigned long long* out) {
+__global__ __launch_bounds__(BLOCK) void digest_kernel(DevParams p, unsigned long long* out) {
     __shared__ unsigned long long part[WAVES_PER_BLOCK];
-    const int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    const int64_t G = p.G;
+    const int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     uint64_t hv = 0;
-    if (i < G) {
-        uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)(p.g0 + i) * 0x9E3779B97F4A7C15ull);
+    if (g < p.G) {
+        uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)(p.g0 + g) * 0x9E3779B97F4A7C15ull);
         auto feed = [&](int32_t v) { h ^= (uint32_t)v; h *= 0x100000001b3ull; };
+        const int s0 = p.gx[GX_S0 * p.G + g];
         for (int r = 0; r < R; ++r) {
-            for (int f = 0; f < RAFT_NUM_FIELDS; ++f) feed(S.st[((int64_t)f * R + r) * G + i]);
-            for (int d = 0; d < R; ++d) feed(S.nx[((int64_t)r * R + d) * G + i]);
-            for (int d = 0; d < R; ++d) feed(S.mt[((int64_t)r * R + d) * G + i]);
-            const int32_t phys = S.st[((int64_t)RAFT_F_PHYS * R + r) * G + i];
-            const uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
-            for (int32_t j = 0; j < phys; ++j) { const uint2 e = lr[j]; feed((int32_t)e.x); feed((int32_t)e.y); }
+            const int64_t idx = g * R + r;
+            for (int f = 0; f < RAFT_NUM_FIELDS; ++f) {
+                const int32_t v = p.st[fidx(p, f, idx)];
+                feed(f == RAFT_F_FLAGS ? (int32_t)((uint32_t)v & FL_EXPORT_MASK) : v);
+            }
+            for (int d = 0; d < R; ++d) feed(canon_next(p, R, g, s0, r, d));
+            for (int d = 0; d < R; ++d) feed(canon_match(p, R, g, s0, r, d));
+            const int32_t phys = p.st[fidx(p, RAFT_F_PHYS, idx)];
+            const uint2* lr = p.log + idx * (int64_t)p.cap;
+            for (int32_t q = 0; q < phys; ++q) { const uint2 e = lr[q]; feed((int32_t)e.x); feed((int32_t)e.y); }
         }
-        feed(S.gx[i]);
-        feed(S.gx[G + i]);
+        feed(p.gx[GX_ISO * p.G + g]);
+        feed(p.gx[GX_CMDS * p.G + g]);
         hv = fmix64(h);
     }
     // wave sum of 64-bit values
@@ -314,8 +332,8 @@ struct RepState {
     __device__ Rep ref() { return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl, t1, t2, c1}; }
 };
 
-__device__ __forceinline__ void load_rep(RepState& x, const DevState& S, int R, int64_t G, int64_t i, int r) {
-#define LD(f) S.st[((int64_t)(f) * R + r) * G + i]
+__device__ __forceinline__ void load_rep(RepState& x, const DevParams& p, int64_t idx) {
+#define LD(f) p.st[fidx(p, f, idx)]
     x.term = LD(RAFT_F_TERM); x.voted = LD(RAFT_F_VOTED); x.role = LD(RAFT_F_ROLE); x.commit = LD(RAFT_F_COMMIT);
     x.last = LD(RAFT_F_LAST); x.phys = LD(RAFT_F_PHYS); x.elec = LD(RAFT_F_ELECTION_MS);
     x.fl = (uint32_t)LD(RAFT_F_FLAGS); x.phase = LD(RAFT_F_PHASE_MS); x.retry = LD(RAFT_F_RETRY_MS);
@@ -330,8 +348,8 @@ __device__ __forceinline__ void derive_cache(RepState& x, const uint2* lr) {
     x.t2 = x.last >= 2 ? (int32_t)lr[x.last - 2].x : 0;
 }
 
-__device__ __forceinline__ void store_rep(const RepState& x, const DevState& S, int R, int64_t G, int64_t i, int r) {
-#define ST(f) S.st[((int64_t)(f) * R + r) * G + i]
+__device__ __forceinline__ void store_rep(const RepState& x, const DevParams& p, int64_t idx) {
+#define ST(f) p.st[fidx(p, f, idx)]
     ST(RAFT_F_TERM) = x.term; ST(RAFT_F_VOTED) = x.voted; ST(RAFT_F_ROLE) = x.role; ST(RAFT_F_COMMIT) = x.commit;
     ST(RAFT_F_LAST) = x.last; ST(RAFT_F_PHYS) = x.phys; ST(RAFT_F_ELECTION_MS) = x.elec;
     ST(RAFT_F_FLAGS) = (int32_t)(x.fl & FL_EXPORT_MASK); ST(RAFT_F_PHASE_MS) = x.phase; ST(RAFT_F_RETRY_MS) = x.retry;
@@ -349,27 +367,28 @@ __device__ __forceinline__ void resolve_rep_draw(RepState& x, const DevParams& p
 enum { BATCH_VOTE = 0, BATCH_APPEND = 1, BATCH_COMMAND = 2 };
 
 // keys[k] = group * R + replica; msgs of key k are order[off[k] .. off[k+1])
-__global__ __launch_bounds__(BLOCK) void batch_kernel(DevState S, DevParams p, uint32_t t, int kind, int nkeys,
+__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int nkeys,
                                                       const int64_t* keys, const int64_t* off, const int64_t* order,
                                                       const void* req, void* resp) {
     const int k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys) return;
     const int R = p.R;
-    const int64_t i = keys[k] / R;
-    const int r = (int)(keys[k] % R);
+    const int64_t idx = keys[k];
+    const int64_t i = idx / R;
+    const int r = (int)(idx % R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
     RepState x;
-    load_rep(x, S, R, p.G, i, r);
-    uint2* lr = p.log + (i * R + r) * (int64_t)p.cap;
+    load_rep(x, p, idx);
+    uint2* lr = p.log + idx * (int64_t)p.cap;
     derive_cache(x, lr);
     Counters cnt;
     cnt.clear();
-    for (int m = off[k]; m < off[k + 1]; ++m) {
+    for (int64_t m = off[k]; m < off[k + 1]; ++m) {
         const int64_t o = order[m];
         if (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt; bool gr;
-            vote_handler(x.ref(), lr, q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
+            vote_handler(x.ref(), q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, gr ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
@@ -385,7 +404,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevState S, DevParams p, u
         }
         resolve_rep_draw(x, p, t, gid, r);
     }
-    store_rep(x, S, R, p.G, i, r);
+    store_rep(x, p, idx);
 }
 
 }  // namespace
@@ -398,12 +417,11 @@ struct raft_engine {
     DevParams dp;
     int device;
     hipStream_t stream;
-    DevState S;
     void* base;
     size_t bytes;
     uint64_t t;
     int K;                      // steps per launch
-    int nblocks;
+    int nblocks;                // step-kernel workgroups: ceil(G / (WAVES_PER_BLOCK * (64 / R)))
     uint32_t* partials;         // [K][NCW][nwaves] packed per-wave counter partials
     int64_t* counters_dev;      // [K][STRIDE] scratch
     // step-kernel event timing
@@ -431,33 +449,28 @@ static void dispatch_R(int R, A&&... a) {
 
 template <int R> struct InitL {
     static void run(raft_engine* e) {
-        const unsigned nb = (unsigned)((e->p.G + BLOCK - 1) / BLOCK);
-        init_kernel<R><<<nb, BLOCK, 0, e->stream>>>(e->S, e->dp);
-    }
-};
-template <int R> struct RebuildL {
-    static void run(raft_engine* e) {
-        rebuild_cache_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->S, e->dp);
+        const unsigned nb = (unsigned)((e->dp.GR + BLOCK - 1) / BLOCK);
+        init_kernel<R><<<nb, BLOCK, 0, e->stream>>>(e->dp);
     }
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
-        step_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->S, e->dp, t0, k, e->partials);
+        step_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->dp, t0, k, e->partials);
     }
 };
 template <int R> struct PackL {
     static void run(raft_engine* e, int64_t g0, int64_t n, int32_t* buf) {
-        pack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->S, e->p.G, g0, n, buf);
+        pack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, g0, n, buf);
     }
 };
 template <int R> struct UnpackL {
     static void run(raft_engine* e, int64_t g0, int64_t n, const int32_t* buf) {
-        unpack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->S, e->p.G, g0, n, buf);
+        unpack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, g0, n, buf);
     }
 };
 template <int R> struct DigestL {
     static void run(raft_engine* e, unsigned long long* out) {
-        digest_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->S, e->dp, out);
+        digest_kernel<R><<<(unsigned)((e->p.G + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, out);
     }
 };
 
@@ -527,17 +540,20 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.churn_thr32 = ppm_thr(p->churn_ppm, 32); d.cmd_thr32 = ppm_thr(p->cmd_ppm, 32);
     d.churn_steps = p->churn_steps; d.part_period = p->partition_period; d.part_len = p->partition_len;
     d.cmd_mode = p->cmd_mode; d.cmd_limit = p->cmd_limit;
-    e->nblocks = (int)((G + BLOCK - 1) / BLOCK);
+    const int64_t gpb = (int64_t)WAVES_PER_BLOCK * (64 / p->R);     // groups per step workgroup
+    e->nblocks = (int)((G + gpb - 1) / gpb);
+    d.GR = G * R;
     e->K = p->steps_per_launch > 0 ? p->steps_per_launch : 1;
 
     const size_t st_b = (size_t)F_DEV * R * G * 4;
-    const size_t ses_b = (size_t)R * R * G * 4;
-    const size_t gx_b = (size_t)2 * G * 4;
+    const size_t ses_b = (size_t)2 * R * G * 4;
+    const size_t spill_b = (size_t)2 * R * R * G * 4;
+    const size_t gx_b = (size_t)GX_WORDS * G * 4;
     const size_t log_b = (size_t)G * R * p->log_cap * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t part_b = (size_t)e->K * NCW * e->nblocks * WAVES_PER_BLOCK * 4;
     const size_t cnt_b = (size_t)e->K * RAFT_COUNTER_STRIDE * 8;
-    e->bytes = al(st_b) + 2 * al(ses_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
+    e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (err != hipSuccess) { delete e; return fail(RAFT_EDEVICE, "hipStreamCreate failed"); }
     err = hipMalloc(&e->base, e->bytes);
@@ -547,16 +563,13 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_ENOMEM, "hipMalloc of " + std::to_string(e->bytes) + " bytes failed");
     }
     char* b = (char*)e->base;
-    e->S.st = (int32_t*)b; b += al(st_b);
-    e->S.nx = (int32_t*)b; b += al(ses_b);
-    e->S.mt = (int32_t*)b; b += al(ses_b);
-    e->S.gx = (int32_t*)b; b += al(gx_b);
+    d.st = (int32_t*)b; b += al(st_b);
+    d.ses = (int32_t*)b; b += al(ses_b);
+    d.spill = (int32_t*)b; b += al(spill_b);
+    d.gx = (int32_t*)b; b += al(gx_b);
     e->partials = (uint32_t*)b; b += al(part_b);
     e->counters_dev = (int64_t*)b; b += al(cnt_b);
-    e->S.log = (uint2*)b;
-    d.log = e->S.log;
-    d.nx = e->S.nx;
-    d.mt = e->S.mt;
+    d.log = (uint2*)b;
     *out = e;
     dispatch_R<InitL>(p->R, e);
     err = hipStreamSynchronize(e->stream);
@@ -585,7 +598,7 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
     if (!e || n_steps < 0) return fail(RAFT_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(e->device));
     if (!e->cache_valid && n_steps > 0) {
-        dispatch_R<RebuildL>(e->p.R, e);
+        rebuild_cache_kernel<<<(unsigned)((e->dp.GR + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp);
         e->cache_valid = true;
     }
     for (int32_t done = 0; done < n_steps;) {
@@ -722,7 +735,7 @@ int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, 
     HIP_TRY(hipSetDevice(e->device));
     const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
     std::vector<uint2> tmp(cnt);
-    HIP_TRY(hipMemcpyAsync(tmp.data(), e->S.log + (size_t)g0 * e->p.R * e->p.log_cap, cnt * 8,
+    HIP_TRY(hipMemcpyAsync(tmp.data(), e->dp.log + (size_t)g0 * e->p.R * e->p.log_cap, cnt * 8,
                            hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     for (size_t k = 0; k < cnt; ++k) { terms[k] = (int32_t)tmp[k].x; cmds[k] = tmp[k].y; }
@@ -738,7 +751,7 @@ int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* 
     std::vector<uint2> tmp(cnt);
     for (size_t k = 0; k < cnt; ++k) tmp[k] = make_uint2((uint32_t)terms[k], cmds[k]);
     e->cache_valid = false;
-    HIP_TRY(hipMemcpyAsync(e->S.log + (size_t)g0 * e->p.R * e->p.log_cap, tmp.data(), cnt * 8,
+    HIP_TRY(hipMemcpyAsync(e->dp.log + (size_t)g0 * e->p.R * e->p.log_cap, tmp.data(), cnt * 8,
                            hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return RAFT_OK;
@@ -794,7 +807,7 @@ static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32
     if (err == hipSuccess) err = hipMemcpyAsync(pq, req, b_req, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) {
         batch_kernel<<<(nk + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
-            e->S, e->dp, (uint32_t)e->t, kind, nk, (const int64_t*)pk, (const int64_t*)po, (const int64_t*)pd, pq,
+            e->dp, (uint32_t)e->t, kind, nk, (const int64_t*)pk, (const int64_t*)po, (const int64_t*)pd, pq,
             resp_sz ? (void*)ps : nullptr);
         err = hipGetLastError();
     }

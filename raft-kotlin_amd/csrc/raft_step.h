@@ -1,23 +1,37 @@
 // raft_step.h — the per-node consensus step of arodionov/raft-kotlin as
-// register-resident SIMT code for gfx950.
+// lane-per-replica SIMT code for gfx950.
 //
-// One lane owns one Raft group: all R replicas' scalar state, the group's
-// primary leader session (nextIndex/matchIndex of one leader) and the step's
-// message temporaries live in VGPRs; replica loops are unrolled against the
-// compile-time R, so the R x R request/response "message tensor" of a phase
-// never exists in memory: a message is a handler call whose arguments are
-// registers of the sender and whose effects land in registers of the
-// receiver.  The logs (the reference's ArrayList, Commons.kt:51) stay in HBM
-// and are touched only at the slots the handlers read or write.
+// Lane mapping.  A wave64 holds GPW = 64 / R whole groups: lane L serves
+// replica r = L % R of group j = L / R (lanes >= GPW * R idle).  Every lane
+// keeps ONE replica's scalar state in VGPRs (RaftServer.kt:35-48: term,
+// votedFor, state, commitIndex, the Log's lastIndex and physical size, the
+// timer and election-loop clocks) plus its column of the group's primary
+// leader session (nextIndex / matchIndex towards this replica,
+// RaftServer.kt:112-113).  The reference's RPC fan-out becomes cross-lane
+// traffic inside the wave:
+//   * a request is a ds_bpermute broadcast of the sender lane's fields to the
+//     group's lanes, and every destination runs its handler IN PARALLEL on its
+//     own registers (one handler per lane instead of R x R unrolled calls);
+//   * responses come back as __ballot bitmasks: the candidate's vote tally is
+//     popcount(ballot(delivered & granted)) (RaftServer.kt:209-211) and the
+//     leader's commit rule (RaftServer.kt:161-162) is a popcount of
+//     ballot(matchIndex > commitIndex) re-evaluated after every acknowledged
+//     entry in destination order.
+// The logs (the reference's ArrayList, Commons.kt:51) stay in HBM; a lane
+// touches only its own replica's slots, plus the leader's slots it is shipped.
 //
-// Leader ticks (phase A) iterate only the lane's *active* sessions (one, in
-// steady state) with the leader index as a per-lane runtime value; the
-// leader's scalars are picked with select chains and the destination loop
-// stays unrolled.  Sessions other than the primary live in their canonical
-// HBM rows and are swapped in when they tick (partitions, stale leaders).
+// Every step follows the lockstep schedule of DESIGN.md §3 (the same schedule
+// the CPU oracle in oracle/raft_oracle.c restates object by object).  The
+// parallel form is exact because (a) a handler only writes its own
+// replica, (b) a sender's self-message never changes the sender's state
+// (its request carries its own snapshot term, which can only be <= its
+// current term), and (c) the sender-side response processing that IS
+// order-dependent (Q6/Q7 term adoption, the +1 commit rule) is replayed in
+// destination order with ballots.
 //
-// The phase order and every tie-break follow DESIGN.md §3 (the same schedule
-// the CPU oracle in oracle/raft_oracle.c restates object by object).
+// Cross-lane rule: every ds_bpermute / ballot that reads another lane runs in
+// control flow that is uniform across a whole group (whole groups are either
+// active or not), so a source lane is never masked off.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "philox.h"
@@ -40,11 +54,27 @@ constexpr uint32_t FL_DRAW = 1u << 5;      // internal: timer re-armed this step
 constexpr uint32_t FL_EXPORT_MASK = ~FL_DRAW;
 constexpr int PEND_SH = RAFT_FL_PENDING_SHIFT, VOTES_SH = RAFT_FL_VOTES_SHIFT, LATCH_SH = RAFT_FL_LATCH_SHIFT;
 
+// engine-internal per-replica fields after the canonical ones: the log-tail
+// cache (term of log[last-1], log[last-2]; cmd of log[last-1])
+constexpr int F_T1 = RAFT_NUM_FIELDS, F_T2 = RAFT_NUM_FIELDS + 1, F_C1 = RAFT_NUM_FIELDS + 2;
+constexpr int F_DEV = RAFT_NUM_FIELDS + 3;
+// group words gx[GX_*][G]
+constexpr int GX_ISO = 0, GX_CMDS = 1, GX_S0 = 2, GX_WORDS = 3;
+
+// HBM layout (all per-replica arrays indexed by idx = g * R + r, so the lanes
+// of a wave read one contiguous run per field):
+//   st    int32 [F_DEV][G*R]        replica scalars + tail cache
+//   ses   int32 [2][G*R]            primary session of group g: nextIndex / matchIndex towards replica r
+//   spill int32 [2][G*R][R]         every other session row: [(g*R + d) * R + s]
+//   gx    int32 [GX_WORDS][G]       isolation word, commands issued, primary-session owner s0 (-1 none)
+//   log   uint2 [G*R][cap]          (term, cmd) physical slots
 struct DevParams {
-    uint2* log;                                // [G][R][cap] (term, cmd)
-    int32_t* nx;                               // [R][R][G] session rows (canonical home)
-    int32_t* mt;                               // [R][R][G]
-    int64_t G, g0;
+    int32_t* st;
+    int32_t* ses;
+    int32_t* spill;
+    int32_t* gx;
+    uint2* log;
+    int64_t G, g0, GR;
     int32_t R, cap;
     uint32_t key0, key1;
     int32_t P, emin, emax, bmin, bmax, round_to, retry;
@@ -57,8 +87,7 @@ struct DevParams {
 struct Entry { int32_t term; uint32_t cmd; };
 
 // Per-lane step counters, two 16-bit counters per register (a lane's count in
-// one step is far below 2^16 / 64, so a wave sum of a packed word cannot
-// carry between halves).
+// one step is < 2^16 / 64, so a wave sum of a packed word cannot carry).
 struct Counters {
     uint32_t w[NCW];
     __device__ __forceinline__ void clear() {
@@ -72,18 +101,7 @@ __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t 
     return philox4x32_10(c0, gid, purpose, sub, p.key0, p.key1);
 }
 
-// Per-(group, step) context.
-struct Ctx {
-    uint32_t t, gid;
-    int64_t i;            // engine-local group index (lane)
-    int32_t iso;          // isolated replica this step, -1 if none
-    uint32_t part;        // replicas on side B of this step's partition
-    uint2* lg;            // this group's log, [R][cap] entries (term, cmd)
-    int cap;
-    Counters* cnt;        // this lane's counters for the step
-};
-
-// One replica's scalar state, by reference into the owning lane's registers.
+// One replica's scalar state, by reference.
 struct Rep {
     int32_t &term, &voted, &role, &commit, &last, &phys, &elec, &phase, &retry;
     uint32_t& fl;
@@ -91,37 +109,10 @@ struct Rep {
     uint32_t& c1;              //                 cmd  of log[last-1]
 };
 
-// Pick / replace element s of a register array for a per-lane runtime s,
-// given as the one-hot mask 1 << s.  Written as masked OR / blend so the
-// optimiser cannot turn it into a dynamically indexed load or store (which
-// would demote the whole register array to scratch memory).
-template <int R>
-__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[R], uint32_t onehot) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) v |= a[r] & (0u - ((onehot >> r) & 1u));
-    return v;
-}
-template <int R>
-__device__ __forceinline__ int32_t pick(const int32_t (&a)[R], uint32_t onehot) {
-    int32_t v = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) v |= a[r] & -(int32_t)((onehot >> r) & 1u);
-    return v;
-}
-template <int R>
-__device__ __forceinline__ void place(int32_t (&a)[R], uint32_t onehot, int32_t v) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int32_t m = -(int32_t)((onehot >> r) & 1u);
-        a[r] = (a[r] & ~m) | (v & m);
-    }
-}
-
 // ---- timer / consumer (Commons.kt:10-31, RaftServer.kt:50-69) -------------
 // reset(): re-arm with a fresh draw.  The draw is a pure function of
-// (step, group, replica), so it is resolved once at the end of the step
-// (resolve_timer_draws) no matter how many resets the step performed.
+// (step, group, replica), so it is resolved once at the end of the step no
+// matter how many resets the step performed (S-9).
 __device__ __forceinline__ void reset_timer(Rep n) { n.fl |= FL_ARMED | FL_DRAW; }
 // launch { channel.send(FOLLOWER) } (RaftServer.kt:241, :261, :266), S-5
 __device__ __forceinline__ void send_follower(Rep n) {
@@ -129,13 +120,12 @@ __device__ __forceinline__ void send_follower(Rep n) {
 }
 
 // ---- Log<T> (Commons.kt:47-74) over one replica's HBM slots ---------------
-// The engine keeps a 2-deep tail cache per replica (t1 = log[last-1].term,
-// t2 = log[last-2].term, c1 = log[last-1].cmd; derived state, never
-// exported).  In steady state every read the handlers make (prev checks,
-// the newest entry, vote last-terms) hits it; HBM is read only for older
-// slots and when the ghost tail resurfaces a stale slot.
-__device__ __forceinline__ int32_t term_at(const uint2* lr, int32_t last, int32_t t1, int32_t t2, int32_t j) {
-    return j == last - 1 ? t1 : j == last - 2 ? t2 : (int32_t)lr[j].x;
+// The 2-deep tail cache answers every steady-state read (prev checks, the
+// newest entry, vote last-terms); HBM is read for older slots and when the
+// ghost tail resurfaces a stale slot.
+__device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t t2, int32_t j, bool& hit) {
+    hit = j == last - 1 || j == last - 2;
+    return j == last - 1 ? t1 : t2;
 }
 
 // Log.add(i, e): 1 true, 0 false, -1 capacity overflow (counted), -2 threw
@@ -165,8 +155,8 @@ __device__ __forceinline__ int log_add(uint2* lr, int cap, Rep n, int32_t i, Ent
 }
 
 // ---- vote() (RaftServer.kt:228-251) ---------------------------------------
-__device__ __forceinline__ void vote_handler(Rep n, const uint2* lr, int32_t rt, int32_t rc, int32_t rli,
-                                             int32_t rlt, Counters& cnt, int32_t& resp_term, bool& granted) {
+__device__ __forceinline__ void vote_handler(Rep n, int32_t rt, int32_t rc, int32_t rli, int32_t rlt, Counters& cnt,
+                                             int32_t& resp_term, bool& granted) {
     granted = false;
     if (rt < n.term) {
     } else if (n.term == rt) {
@@ -229,397 +219,475 @@ __device__ __forceinline__ void append_command(Rep n, uint2* lr, int cap, uint32
 }
 
 // ---------------------------------------------------------------------------
-// The register-resident group.
+// Lane-per-replica machinery
 // ---------------------------------------------------------------------------
-template <int R>
-struct Group {
-    int32_t term[R], voted[R], role[R], commit[R], last[R], phys[R], elec[R], phase[R], retry[R];
-    uint32_t fl[R];
-    int32_t t1[R], t2[R];           // log-tail cache (terms of log[last-1], log[last-2])
-    uint32_t c1[R];                 //                (cmd of log[last-1])
-    int32_t s0;                     // owner of the primary session in registers, -1 none
-    int32_t nx0[R], mc0[R];         // its nextIndex / matchIndex (RaftServer.kt:112-113)
-    int32_t iso, cmdc;              // harness: isolation word, commands issued
+__device__ __forceinline__ int32_t bcast(int32_t v, int src_lane) {
+    return __builtin_amdgcn_ds_bpermute(src_lane << 2, v);
+}
+__device__ __forceinline__ uint32_t bcastu(uint32_t v, int src_lane) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int32_t)v);
+}
 
-    __device__ __forceinline__ Rep rep(int r) {
-        return Rep{term[r], voted[r], role[r], commit[r], last[r], phys[r], elec[r], phase[r], retry[r], fl[r],
-                   t1[r], t2[r], c1[r]};
+// One lane's replica plus the group words every lane of the group replicates.
+struct Node {
+    int32_t term, voted, role, commit, last, phys, elec, phase, retry;
+    uint32_t fl;
+    int32_t t1, t2;
+    uint32_t c1;
+    int32_t nx, mc;           // primary session (owner s0) towards this replica
+    int32_t iso, cmdc, s0;    // group words
+    __device__ __forceinline__ Rep rep() {
+        return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl, t1, t2, c1};
     }
 };
 
-// primary-session spill / fill (canonical HBM rows nx/mt[s][d][G])
 template <int R>
-__device__ __forceinline__ void session_store(const Group<R>& g, const DevParams& p, int64_t i) {
-#pragma unroll
-    for (int d = 0; d < R; ++d) {
-        p.nx[((int64_t)g.s0 * R + d) * p.G + i] = g.nx0[d];
-        p.mt[((int64_t)g.s0 * R + d) * p.G + i] = g.mc0[d];
+struct Lanes {
+    static constexpr int GPW = 64 / R;                 // groups per wave
+    static constexpr uint32_t ALL = (1u << R) - 1u;
+    static constexpr int MAJ = R / 2 + 1;              // RaftServer.kt:44
+    static constexpr int NQ = (R + 3) / 4;             // Philox calls per 4-replica quad
+    static constexpr bool JOBS = 1 + 2 * NQ <= R;      // per-step draws fit one lane each
+
+    // lanes whose replica index is s (compile-time masks)
+    static constexpr uint64_t lanes_of(int s) {
+        uint64_t m = 0;
+        for (int j = 0; j < GPW; ++j) m |= 1ull << (j * R + s);
+        return m;
     }
-}
+};
+
+// Per-lane, per-step context.
 template <int R>
-__device__ __forceinline__ void session_load(Group<R>& g, const DevParams& p, int64_t i, int s) {
-    g.s0 = s;
-#pragma unroll
-    for (int d = 0; d < R; ++d) {
-        g.nx0[d] = p.nx[((int64_t)s * R + d) * p.G + i];
-        g.mc0[d] = p.mt[((int64_t)s * R + d) * p.G + i];
+struct Ctx {
+    uint32_t t, gid;
+    int r, base;              // replica index, first lane of the group
+    bool live;                // lane holds a real replica (whole groups are live or not)
+    int64_t idx;              // g * R + r
+    int iso;                  // isolated replica this step, -1 if none
+    uint32_t part;            // replicas on side B of this step's partition
+    uint2* lr;                // this replica's log
+    u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS)
+
+    __device__ __forceinline__ uint32_t gbits(uint64_t b) const {
+        return (uint32_t)(b >> base) & Lanes<R>::ALL;
+    }
+    __device__ __forceinline__ int src(int s) const { return base + s; }
+};
+
+template <int R>
+__device__ __forceinline__ bool lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
+    if (s == d) return false;                                      // S-7
+    if (c.iso >= 0 && (s == c.iso || d == c.iso)) return true;
+    if (((c.part >> s) ^ (c.part >> d)) & 1u) return true;
+    if (p.drop_thr16 == 0) return false;
+    return ((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16;             // uniform j = 2*dd + b: word dd, half b
+}
+
+// 16-bit drop uniforms of sender s for this lane as destination d (S-9):
+// word dd = (d < s ? d : d - 1) of Philox(t, gid, purpose, s | (dd >> 2) << 8).
+// Every lane of the group evaluates it for its own dd, so one Philox
+// evaluation of the wave serves every destination.
+template <int R>
+__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s) {
+    if (p.drop_thr16 == 0) return 0u;
+    const int dd = c.r < s ? c.r : c.r - 1;
+    const int q = dd < 0 ? 0 : dd;
+    const u32x4 w = draw(p, c.t, c.gid, purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
+    return word_of(w, q & 3);
+}
+
+// The step's per-(group, replica) timer / backoff draw word for this lane,
+// word r & 3 of Philox(t, gid, purpose, r >> 2).  With JOBS the group's lanes
+// computed them at step start: lane 1 + q holds timer quad q, lane 1 + NQ + q
+// backoff quad q.  MUST be called in group-uniform control flow.
+template <int R>
+__device__ __forceinline__ uint32_t quad_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose) {
+    if constexpr (Lanes<R>::JOBS) {
+        const int first = purpose == RAFT_RNG_TIMER ? 1 : 1 + Lanes<R>::NQ;
+        const int sl = c.src(first + (c.r >> 2));
+        const uint32_t a = bcastu(c.job.x, sl), b = bcastu(c.job.y, sl);
+        const uint32_t x = bcastu(c.job.z, sl), y = bcastu(c.job.w, sl);
+        const int k = c.r & 3;
+        return k == 0 ? a : k == 1 ? b : k == 2 ? x : y;
+    } else {
+        return word_of(draw(p, c.t, c.gid, purpose, (uint32_t)(c.r >> 2)), c.r & 3);
     }
 }
 
 template <int R>
 struct Stepper {
-    static constexpr int MAJ = R / 2 + 1;              // RaftServer.kt:44
-    static constexpr uint32_t ALL = (1u << R) - 1u;
+    using L = Lanes<R>;
+    static constexpr int MAJ = L::MAJ;
+    static constexpr uint32_t ALL = L::ALL;
 
-    // vote request snapshot of sender s (S-4); send mask per sender
-    int32_t qt[R], qli[R], qlt[R];
-    uint32_t send[R];
-
-    // 16-bit drop uniform j = 2*dd + b of sender s (S-9); s may be a runtime value
-    __device__ __forceinline__ static bool lost(const DevParams& p, const Ctx& c, const u32x4* du, int s, int d, int b) {
-        if (s == d) return false;                                      // S-7
-        if (c.iso >= 0 && (s == c.iso || d == c.iso)) return true;
-        if (((c.part >> s) ^ (c.part >> d)) & 1u) return true;
-        if (p.drop_thr16 == 0) return false;
-        const int dd = d < s ? d : d - 1;
-        const int j = 2 * dd + b;                   // 0 .. 2R-3 < 16
-        // word j >> 1 of the 8-word (du[0], du[1]) pair, by one-hot masks (no
-        // dynamic indexing: it would demote du to scratch)
-        const uint32_t oh = 1u << (j >> 1);
-        const uint32_t w8[8] = {du[0].x, du[0].y, du[0].z, du[0].w, du[1].x, du[1].y, du[1].z, du[1].w};
-        uint32_t word = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) word |= w8[k] & (0u - ((oh >> k) & 1u));
-        return ((word >> (16 * (j & 1))) & 0xFFFFu) < p.drop_thr16;
+    // ---- session rows (S-8): the primary lives in n.nx / n.mc, the others in spill
+    __device__ __forceinline__ static void spill_store(const DevParams& p, const Ctx<R>& c, const Node& n, int s) {
+        p.spill[c.idx * R + s] = n.nx;
+        p.spill[p.GR * R + c.idx * R + s] = n.mc;
+    }
+    __device__ __forceinline__ static void spill_load(const DevParams& p, const Ctx<R>& c, Node& n, int s) {
+        n.nx = p.spill[c.idx * R + s];
+        n.mc = p.spill[p.GR * R + c.idx * R + s];
     }
 
-    __device__ __forceinline__ static void drop_uniforms(const DevParams& p, const Ctx& c, uint32_t purpose, int s, u32x4* du) {
-        du[0] = draw(p, c.t, c.gid, purpose, (uint32_t)s);
-        if (2 * (R - 1) > 8) du[1] = draw(p, c.t, c.gid, purpose, (uint32_t)s | (1u << 8));
-        else du[1] = du[0];
+    // while (state == CANDIDATE) iteration head (RaftServer.kt:191-199): the
+    // RequestVote snapshot is built inside retry{} (:200-207)
+    __device__ __forceinline__ static void build_vote_request(Node& n, Counters& cnt, int32_t& qt, int32_t& qli,
+                                                              int32_t& qlt) {
+        qt = n.term;
+        qli = n.last;
+        qlt = 0;
+        if (n.last != 0) { qlt = n.t1; cnt.add(RAFT_C_VOTE_LOG_READS); }
+    }
+    __device__ __forceinline__ static void start_round(Node& n, int r, Counters& cnt, uint32_t& send, int32_t& qt,
+                                                       int32_t& qli, int32_t& qlt) {
+        n.term += 1;                                                      // :192
+        n.voted = r + 1;                                                  // :193
+        n.fl = (n.fl & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
+               (ALL << PEND_SH);
+        n.phase = 0;
+        n.retry = 0;
+        send = ALL;
+        build_vote_request(n, cnt, qt, qli, qlt);
+        cnt.add(RAFT_C_ROUNDS);
     }
 
-    // RequestVote snapshot built inside retry{} (RaftServer.kt:200-207)
-    __device__ __forceinline__ void build_vote_request(Group<R>& g, const Ctx& c, int r) {
-        qt[r] = g.term[r];
-        qli[r] = g.last[r];
-        if (g.last[r] == 0) qlt[r] = 0;
-        else {
-            qlt[r] = g.t1[r];                                  // log.get(lastIndex - 1).term
-            c.cnt->add(RAFT_C_VOTE_LOG_READS);
-        }
-    }
-
-    // while (state == CANDIDATE) iteration head (RaftServer.kt:191-199)
-    __device__ __forceinline__ void start_round(Group<R>& g, const Ctx& c, int r) {
-        g.term[r] += 1;
-        g.voted[r] = r + 1;
-        g.fl[r] = (g.fl[r] & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
-                  (ALL << PEND_SH);
-        g.phase[r] = 0;
-        g.retry[r] = 0;
-        send[r] = ALL;
-        build_vote_request(g, c, r);
-        c.cnt->add(RAFT_C_ROUNDS);
-    }
-
-    // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113), S-8.
-    // The primary slot is taken over; the previous owner's row goes home.
-    __device__ __forceinline__ static void start_session(Group<R>& g, const DevParams& p, const Ctx& c, int r) {
-        g.fl[r] |= FL_HB;
-        if (g.s0 >= 0 && g.s0 != r) session_store<R>(g, p, c.i);
-        g.s0 = r;
-#pragma unroll
-        for (int d = 0; d < R; ++d) { g.nx0[d] = g.commit[r] + 1; g.mc0[d] = 0; }
-        c.cnt->add(RAFT_C_LEADERS_ELECTED);
-    }
-
-    // leaderElection() returns; queued sends then the final state (S-5)
-    __device__ __forceinline__ static void end_election(Group<R>& g, const DevParams& p, const Ctx& c, int r) {
-        uint32_t f = g.fl[r];
+    // leaderElection() returns; queued sends then the final state (S-5).
+    // Returns true when the final state is LEADER: the caller starts the
+    // heartbeat session (RaftServer.kt:66) in group order.
+    __device__ __forceinline__ static bool end_election(Node& n) {
+        uint32_t f = n.fl;
         const bool prst = f & FL_PRST;
         f &= ~(FL_ELECTING | FL_PRST | FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH));
         if (prst) f |= FL_ARMED | FL_DRAW;
-        g.fl[r] = f;
-        g.phase[r] = 0;
-        g.retry[r] = 0;
-        if (g.role[r] == RAFT_LEADER) start_session(g, p, c, r);             // :66
-        else if (g.role[r] == RAFT_FOLLOWER) g.fl[r] |= FL_ARMED | FL_DRAW;  // :64
+        n.fl = f;
+        n.phase = 0;
+        n.retry = 0;
+        if (n.role == RAFT_LEADER) { n.fl |= FL_HB; return true; }       // :66
+        if (n.role == RAFT_FOLLOWER) n.fl |= FL_ARMED | FL_DRAW;         // :64
+        return false;
     }
 
-    // One fixedRateTimer tick of leader s (RaftServer.kt:115-176); s is a
-    // per-lane runtime index.  Requests are all built before any handler runs
-    // (S-4); responses are processed in dst order on a working copy of the
-    // leader's scalars, written back at the end.  The self-handler (d == s)
-    // only ever touches s's log, lastIndex and physLen (its request carries
-    // leaderId == id and the tick-start term and commit), so the copy and the
-    // registers never disagree on anything a handler reads.
-    __device__ __forceinline__ static void tick(Group<R>& g, const DevParams& p, Ctx& c, int s) {
-        Counters& cnt = *c.cnt;
-        const uint32_t oh = 1u << s;
-        if (pick(g.role, oh) == RAFT_FOLLOWER) {                      // :117 cancel() (S-10)
+    // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113) for every
+    // lane with `starting`, in ascending replica order within a group: each
+    // start takes over the primary slot, the previous owner's row goes to spill.
+    // Called in wave-uniform control flow.
+    __device__ __forceinline__ static void start_sessions(const DevParams& p, const Ctx<R>& c, Node& n, bool starting,
+                                                          Counters& cnt) {
+        const uint64_t b = __ballot(starting);
+        if (b == 0) return;
+        if (starting) cnt.add(RAFT_C_LEADERS_ELECTED);
+        const uint32_t sb = c.gbits(b);
 #pragma unroll
-            for (int r = 0; r < R; ++r) g.fl[r] &= ~(((oh >> r) & 1u) * FL_HB);
+        for (int s = 0; s < R; ++s) {
+            if (!(b & L::lanes_of(s))) continue;                          // wave-uniform
+            const int32_t cs = bcast(n.commit, c.src(s));
+            if ((sb >> s) & 1u) {                                         // group-uniform
+                if (n.s0 >= 0 && n.s0 != s) spill_store(p, c, n, n.s0);
+                n.s0 = s;
+                n.nx = cs + 1;                                            // :112
+                n.mc = 0;                                                 // :113
+            }
+        }
+    }
+
+    // One fixedRateTimer tick of leader s (RaftServer.kt:115-176) in every
+    // group of the active lanes (group-uniform s, runtime).  Requests are built
+    // from the leader's tick-start snapshot (S-4) and delivered to all
+    // destinations at once; responses are replayed in destination order.
+    __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, int s, Counters& cnt) {
+        const int sl = c.src(s);
+        const int32_t role_s = bcast(n.role, sl);
+        if (role_s == RAFT_FOLLOWER) {                                    // :117 cancel() (S-10)
+            if (c.r == s) n.fl &= ~FL_HB;
             return;
         }
-        cnt.add(RAFT_C_SESSIONS_TICKED);
-        if (s != g.s0) {                                               // swap the session in
-            if (g.s0 >= 0) session_store<R>(g, p, c.i);
-            session_load<R>(g, p, c.i, s);
+        if (c.r == s) cnt.add(RAFT_C_SESSIONS_TICKED);
+        if (n.s0 != s) {                                                  // swap the session in
+            if (n.s0 >= 0) spill_store(p, c, n, n.s0);
+            spill_load(p, c, n, s);
+            n.s0 = s;
         }
-        const int32_t Lterm = pick(g.term, oh), Lcommit = pick(g.commit, oh), Llast = pick(g.last, oh);
-        const int32_t Lt1 = pick(g.t1, oh), Lt2 = pick(g.t2, oh), Lc1 = (int32_t)pick(g.c1, oh);
-        const uint2* ls = c.lg + s * c.cap;
-        // Every log slot this tick reads is resolved up front: the leader's
-        // log[prev] and log[i-1] for each request (built before any handler
-        // runs, RaftServer.kt:122-132) and each follower's own log[prev]
-        // (append() :274-276).  The tail cache answers the steady-state ones;
-        // the rest are loaded in one batch.  A handler only writes its own
-        // replica's log, so no earlier handler of the tick can change a slot a
-        // later one reads.
-        int32_t lpt[R], dpt[R];
-        uint2 lent[R];
-#pragma unroll
-        for (int d = 0; d < R; ++d) {
-            const int32_t i = g.nx0[d], prev = i - 2;
-            lpt[d] = (prev >= 0 && prev <= Llast - 1) ? term_at(ls, Llast, Lt1, Lt2, prev) : -1;
-            lent[d] = (i >= 1 && i <= Llast) ? (i == Llast ? make_uint2((uint32_t)Lt1, (uint32_t)Lc1) : ls[i - 1])
-                                             : make_uint2(0u, 0u);
-            const uint2* lr = c.lg + d * c.cap;
-            dpt[d] = (prev >= 0 && prev < g.last[d]) ? term_at(lr, g.last[d], g.t1[d], g.t2[d], prev) : 0;
+        const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
+        const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
+        const uint32_t Lc1 = bcastu(n.c1, sl);
+
+        // build this destination's request (RaftServer.kt:122-132)
+        const int32_t i = n.nx, prev = i - 2;
+        bool ok = true, has = false;
+        if (prev >= 0) {                                                  // :128 (Q11)
+            if (prev > Llast - 1) ok = false;
+            else cnt.add(RAFT_C_PREV_READS_LEADER);
         }
-        // build every request (RaftServer.kt:122-132)
-        uint32_t okm = 0, hasm = 0;
-#pragma unroll
-        for (int d = 0; d < R; ++d) {
-            const int32_t i = g.nx0[d], prev = i - 2;
-            bool ok = true;
-            if (prev >= 0) {                                           // :128 (Q11)
-                if (prev > Llast - 1) ok = false;
-                else cnt.add(RAFT_C_PREV_READS_LEADER);
-            }
-            if (ok && Llast >= i) {                                    // :130-131
-                if (i - 1 < 0) ok = false;
-                else { hasm |= 1u << d; cnt.add(RAFT_C_ENTRY_READS_LEADER); }
-            }
-            if (ok) okm |= 1u << d;
-            else cnt.add(RAFT_C_APPEND_SKIPPED);
+        if (ok && Llast >= i) {                                           // :130-131
+            if (i - 1 < 0) ok = false;
+            else { has = true; cnt.add(RAFT_C_ENTRY_READS_LEADER); }
         }
-        u32x4 du[2];
-        if (p.drop_thr16) drop_uniforms(p, c, RAFT_RNG_APPEND_DROP, s, du);
-        int32_t T = Lterm, C = Lcommit;
-        bool stepdown = false;
-#pragma unroll
-        for (int d = 0; d < R; ++d) {
-            if (!((okm >> d) & 1u)) continue;
+        if (!ok) cnt.add(RAFT_C_APPEND_SKIPPED);
+        // every log slot of the tick, resolved up front: the leader's log[prev]
+        // and log[i-1], and this replica's own log[prev] (append() :274-276);
+        // a handler only writes its own replica's log, so no handler of the
+        // tick can change a slot another one reads.
+        const uint2* ls = c.lr + (int64_t)(s - c.r) * p.cap;
+        bool h1, h2;
+        int32_t lpt = cached_term(Llast, Lt1, Lt2, prev, h1);
+        int32_t dpt = cached_term(n.last, n.t1, n.t2, prev, h2);
+        uint2 lent = make_uint2((uint32_t)Lt1, Lc1);
+        const bool ld1 = ok && prev >= 0 && !h1;
+        const bool ld2 = ok && has && i != Llast;
+        const bool ld3 = ok && prev >= 0 && prev < n.last && !h2;
+        if (ld1) lpt = (int32_t)ls[prev].x;
+        if (ld2) lent = ls[i - 1];
+        if (ld3) dpt = (int32_t)c.lr[prev].x;
+
+        const uint32_t dw = drop_word(p, c, RAFT_RNG_APPEND_DROP, s);
+        bool lreq = false, lresp = false, delivered = false, succ = false;
+        int32_t rterm = 0;
+        if (ok) {
             cnt.add(RAFT_C_APPEND_SENT);
-            if (lost(p, c, du, s, d, 0)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }   // :170-172
-            const int32_t prev = g.nx0[d] - 2;
-            const bool has = (hasm >> d) & 1u;
-            int32_t rterm; bool succ;
-            if (!append_handler(g.rep(d), d + 1, c.lg + d * c.cap, c.cap, Lterm, s + 1, prev, lpt[d], has,
-                                Entry{(int32_t)lent[d].x, lent[d].y}, Lcommit, dpt[d], cnt, rterm, succ))
-                continue;
-            if (lost(p, c, du, s, d, 1)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
-            if (rterm > T) { T = rterm; stepdown = true; continue; }  // :146-154 (Q7)
-            if (succ) {                                                // :156-165 (Q9)
-                if (has) {
-                    g.nx0[d] += 1;
-                    g.mc0[d] += 1;
-                    cnt.add(RAFT_C_ENTRIES_ACKED);
-                    int k = 0;
-#pragma unroll
-                    for (int q = 0; q < R; ++q) k += g.mc0[q] > C;     // :161
-                    if (k >= MAJ) { C += 1; cnt.add(RAFT_C_COMMITS); } // :162
-                } else {
-                    g.mc0[d] = prev + 1;                               // :164
+            lreq = lost(p, c, s, c.r, dw, 0);                             // :170-172
+            if (!lreq) {
+                if (append_handler(n.rep(), c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
+                                   Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ)) {
+                    lresp = lost(p, c, s, c.r, dw, 1);
+                    delivered = !lresp;
                 }
-            } else {
-                g.nx0[d] -= 1;                                         // :167
             }
         }
-        place(g.term, oh, T);
-        place(g.commit, oh, C);
-        if (stepdown) {                                                // :148 + offer(FOLLOWER) :152 (S-6)
-            place(g.role, stepdown ? oh : 0u, RAFT_FOLLOWER);
+        if (lreq | lresp) cnt.add(RAFT_C_MSG_DROPPED);
+
+        // responses in destination order (S-4).  :146-154 (Q7): a response
+        // with a term above the running term adopts it and skips the rest of
+        // that response; the running term is the prefix max.
+        int32_t T = Lterm;
+        bool sdb = false;                                                 // this response stepped down
+        const uint64_t hib = __ballot(delivered && rterm > Lterm);
+        const bool stepdown = c.gbits(hib) != 0;
+        if (hib) {                                                        // wave-uniform, rare
+            const uint32_t dl = c.gbits(__ballot(delivered));
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (((oh >> r) & 1u) && !(g.fl[r] & FL_ELECTING)) g.fl[r] |= FL_ARMED | FL_DRAW;
+            for (int q = 0; q < R; ++q) {
+                const int32_t rq = bcast(rterm, c.src(q));
+                if (((dl >> q) & 1u) && rq > T) { T = rq; if (c.r == q) sdb = true; }
+            }
+        }
+        const int32_t mc_old = n.mc;
+        bool chk = false;
+        if (delivered && !sdb) {
+            if (succ) {                                                   // :156-165 (Q9)
+                if (has) { n.nx += 1; n.mc += 1; cnt.add(RAFT_C_ENTRIES_ACKED); chk = true; }
+                else n.mc = prev + 1;                                     // :164
+            } else {
+                n.nx -= 1;                                                // :167
+            }
+        }
+        // commit rule, after each acknowledged entry in destination order:
+        // count(matchIndex > commitIndex) >= majority => commitIndex += 1
+        int32_t C = Lcommit;
+        const uint64_t ckb = __ballot(chk);
+        if (ckb) {                                                        // wave-uniform
+            const uint32_t ck = c.gbits(ckb);
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                if (!(ckb & L::lanes_of(q))) continue;                    // wave-uniform
+                const int32_t cur = c.r <= q ? n.mc : mc_old;             // rows after / before response q
+                const uint32_t gt = c.gbits(__ballot(cur > C));           // :161
+                if (((ck >> q) & 1u) && __popc(gt) >= MAJ) {              // :162
+                    C += 1;
+                    if (c.r == q) cnt.add(RAFT_C_COMMITS);
+                }
+            }
+        }
+        if (c.r == s) {
+            n.term = T;
+            n.commit = C;
+            if (stepdown) {                                               // :148 + offer(FOLLOWER) :152 (S-6)
+                n.role = RAFT_FOLLOWER;
+                if (!(n.fl & FL_ELECTING)) n.fl |= FL_ARMED | FL_DRAW;
+            }
         }
     }
 
-    __device__ __forceinline__ void step(Group<R>& g, const DevParams& p, Ctx& c) {
-        Counters& cnt = *c.cnt;
-        // ---------------- H: harness ----------------
-        u32x4 hw = u32x4{0u, 0u, 0u, 0u};
-        if (p.churn_thr32 | p.cmd_thr32) hw = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
-        {
-            int32_t rem = g.iso >> 8, rep = g.iso & 0xFF;
-            if (rem > 0) { rem--; if (rem == 0) rep = 0; }
-            if (p.churn_thr32 && p.churn_steps > 0 && rem == 0 && hw.x < p.churn_thr32) {
-                int L = -1;
-#pragma unroll
-                for (int r = R - 1; r >= 0; --r) if (g.role[r] == RAFT_LEADER) L = r;
-                if (L >= 0) { rep = L; rem = p.churn_steps; }
-            }
-            g.iso = rem > 0 ? (rem << 8) | rep : 0;
-            c.iso = rem > 0 ? rep : -1;
+    // One lockstep step of every group of the wave.
+    // Called by all 64 lanes (converged); `n` of a dead lane is inert.
+    __device__ __forceinline__ static void step(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt) {
+        const int r = c.r;
+        // ---------------- per-step Philox jobs (S-9) ----------------
+        // lane 0 of a group: harness; lanes 1..NQ: timer quads; lanes
+        // NQ+1..2NQ: backoff quads.  One Philox evaluation of the wave.
+        uint32_t hw0, hw1, hw2;
+        if constexpr (L::JOBS) {
+            const uint32_t purpose = r == 0 ? RAFT_RNG_HARNESS : r <= L::NQ ? RAFT_RNG_TIMER : RAFT_RNG_BACKOFF;
+            const uint32_t sub = r == 0 ? 0u : r <= L::NQ ? (uint32_t)(r - 1) : (uint32_t)(r - 1 - L::NQ);
+            c.job = draw(p, c.t, c.gid, purpose, sub);
+            hw0 = bcastu(c.job.x, c.base);
+            hw1 = bcastu(c.job.y, c.base);
+            hw2 = bcastu(c.job.z, c.base);
+        } else {
+            const u32x4 h = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
+            hw0 = h.x; hw1 = h.y; hw2 = h.z;
         }
-        c.part = 0;
-        if (p.part_period > 0) {
-            const uint32_t ph = c.t % (uint32_t)p.part_period;
-            if ((int64_t)ph < p.part_len) c.part = draw(p, c.t - ph, c.gid, RAFT_RNG_PARTITION, 0).x & ALL;
+
+        // ---------------- H: harness ----------------
+        {
+            int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
+            if (rem > 0) { rem--; if (rem == 0) rep = 0; }
+            const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
+            if (p.churn_thr32 && p.churn_steps > 0 && rem == 0 && hw0 < p.churn_thr32 && lead) {
+                rep = __builtin_ctz(lead);                                  // lowest-id LEADER
+                rem = p.churn_steps;
+            }
+            n.iso = rem > 0 ? (rem << 8) | rep : 0;
+            c.iso = rem > 0 ? rep : -1;
         }
 
         // ---------------- T: timers and election clocks ----------------
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            send[r] = 0;
+        uint32_t send = 0;
+        int32_t qt = 0, qli = 0, qlt = 0;
+        bool sstart = false;
+        {
             bool started = false;
-            if (g.fl[r] & FL_ARMED) {
-                g.elec[r] -= p.P;
-                if (g.elec[r] <= 0) {                                   // Commons.kt:25-27
-                    g.fl[r] &= ~FL_ARMED;
-                    g.elec[r] = 0;
+            if (n.fl & FL_ARMED) {
+                n.elec -= p.P;
+                if (n.elec <= 0) {                                          // Commons.kt:25-27
+                    n.fl &= ~FL_ARMED;
+                    n.elec = 0;
                     cnt.add(RAFT_C_TIMEOUTS);
-                    g.role[r] = RAFT_CANDIDATE;                         // RaftServer.kt:182
-                    if (!(g.fl[r] & FL_ELECTING)) {                     // :184 -> :65
-                        g.fl[r] |= FL_ELECTING;
-                        start_round(g, c, r);
+                    n.role = RAFT_CANDIDATE;                                // RaftServer.kt:182
+                    if (!(n.fl & FL_ELECTING)) {                            // :184 -> :65
+                        n.fl |= FL_ELECTING;
+                        start_round(n, r, cnt, send, qt, qli, qlt);
                         started = true;
                     }
                 }
             }
-            if ((g.fl[r] & FL_ELECTING) && !started) {
-                if (!(g.fl[r] & FL_BACKOFF)) {
-                    g.phase[r] += p.P;                                  // latch clock :214
-                    const uint32_t pend = (g.fl[r] >> PEND_SH) & 0xFFu;
-                    if (pend && g.phase[r] < p.round_to) {
-                        g.retry[r] -= p.P;                              // Commons.kt:43
-                        if (g.retry[r] <= 0) { build_vote_request(g, c, r); send[r] = pend; }
+            if ((n.fl & FL_ELECTING) && !started) {
+                if (!(n.fl & FL_BACKOFF)) {
+                    n.phase += p.P;                                         // latch clock :214
+                    const uint32_t pend = (n.fl >> PEND_SH) & 0xFFu;
+                    if (pend && n.phase < p.round_to) {
+                        n.retry -= p.P;                                     // Commons.kt:43
+                        if (n.retry <= 0) { build_vote_request(n, cnt, qt, qli, qlt); send = pend; }
                     }
                 } else {
-                    g.phase[r] -= p.P;                                  // delay(backoff) :221
-                    if (g.phase[r] <= 0) {
-                        if (g.role[r] == RAFT_CANDIDATE) start_round(g, c, r);   // :191
-                        else end_election(g, p, c, r);
+                    n.phase -= p.P;                                         // delay(backoff) :221
+                    if (n.phase <= 0) {
+                        if (n.role == RAFT_CANDIDATE) start_round(n, r, cnt, send, qt, qli, qlt);   // :191
+                        else sstart = end_election(n);
                     }
                 }
             }
         }
+        start_sessions(p, c, n, sstart, cnt);
 
         // ---------------- V: RequestVote fan-out (S-3) ----------------
-        bool anysend = false;
-#pragma unroll
-        for (int s = 0; s < R; ++s) anysend |= send[s] != 0;
-        if (__any(anysend)) {
+        const uint64_t sendb = __ballot(send != 0);
+        if (sendb) {
 #pragma unroll
             for (int s = 0; s < R; ++s) {
-                if (!__any(send[s] != 0)) continue;
-                u32x4 du[2];
-                if (p.drop_thr16 && send[s]) drop_uniforms(p, c, RAFT_RNG_VOTE_DROP, s, du);
-                if (send[s]) {
-#pragma unroll
-                    for (int d = 0; d < R; ++d) {
-                        if (!((send[s] >> d) & 1u)) continue;
-                        if (lost(p, c, du, s, d, 0)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
-                        int32_t rterm; bool granted;
-                        vote_handler(g.rep(d), c.lg + d * c.cap, qt[s], s + 1, qli[s], qlt[s], cnt, rterm, granted);
-                        if (lost(p, c, du, s, d, 1)) { cnt.add(RAFT_C_MSG_DROPPED); continue; }
-                        uint32_t f = g.fl[s];
-                        f &= ~(1u << (PEND_SH + d));
-                        f += 1u << LATCH_SH;                              // :209
-                        if (granted) f += 1u << VOTES_SH;                 // :211
-                        g.fl[s] = f;
-                        if (g.term[s] < rterm) g.role[s] = RAFT_FOLLOWER; // :210 (Q6)
+                if (!(sendb & L::lanes_of(s))) continue;                    // wave-uniform
+                const int sl = c.src(s);
+                const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
+                const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
+                const int32_t st = bcast(n.term, sl);
+                const uint32_t dw = drop_word(p, c, RAFT_RNG_VOTE_DROP, s);
+                bool lreq = false, lresp = false, delivered = false, granted = false;
+                int32_t rterm = 0;
+                if (c.live && ((ms >> r) & 1u)) {
+                    lreq = lost(p, c, s, r, dw, 0);                         // retry{} swallows, Commons.kt:41
+                    if (!lreq) {
+                        vote_handler(n.rep(), rt, s + 1, rli, rlt, cnt, rterm, granted);
+                        lresp = lost(p, c, s, r, dw, 1);
+                        delivered = !lresp;
                     }
-                    send[s] = 0;
-                    if ((g.fl[s] >> PEND_SH) & 0xFFu) g.retry[s] = p.retry;
+                }
+                if (lreq | lresp) cnt.add(RAFT_C_MSG_DROPPED);
+                // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
+                const uint32_t dl = c.gbits(__ballot(delivered));
+                const uint32_t gr = c.gbits(__ballot(delivered && granted));
+                const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
+                if (r == s && ms) {
+                    uint32_t f = n.fl & ~(dl << PEND_SH);
+                    f += (uint32_t)__popc(dl) << LATCH_SH;                  // :209 countDown()
+                    f += (uint32_t)__popc(gr) << VOTES_SH;                  // :211
+                    n.fl = f;
+                    if (hi) n.role = RAFT_FOLLOWER;                         // :210 (Q6)
+                    if ((f >> PEND_SH) & 0xFFu) n.retry = p.retry;
                 }
             }
         }
 
         // ---------------- D: latch closes -> decision (RaftServer.kt:214-222) ----------------
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t f = g.fl[r];
-            if (!(f & FL_ELECTING) || (f & FL_BACKOFF)) continue;
+        bool dstart = false, need_bo = false;
+        {
+            const uint32_t f = n.fl;
             const int latch = (f >> LATCH_SH) & 0xF, votes = (f >> VOTES_SH) & 0xF;
-            if (latch < MAJ && g.phase[r] < p.round_to) continue;
-            g.fl[r] = f & ~(0xFFu << PEND_SH);                          // cancelChildren() :215
-            if (g.role[r] == RAFT_CANDIDATE && votes >= MAJ) {          // :218-219
-                g.role[r] = RAFT_LEADER;
-                end_election(g, p, c, r);
-            } else if (g.role[r] == RAFT_CANDIDATE) {                   // :220-221
-                g.fl[r] = (g.fl[r] & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
-                const u32x4 w = draw(p, c.t, c.gid, RAFT_RNG_BACKOFF, (uint32_t)(r >> 2));
-                g.phase[r] = scale_range(word_of(w, r & 3), p.bmin, p.bmax);
-                g.retry[r] = 0;
-            } else {
-                end_election(g, p, c, r);
+            if ((f & FL_ELECTING) && !(f & FL_BACKOFF) && (latch >= MAJ || n.phase >= p.round_to)) {
+                n.fl = f & ~(0xFFu << PEND_SH);                             // cancelChildren() :215
+                if (n.role == RAFT_CANDIDATE && votes >= MAJ) {             // :218-219
+                    n.role = RAFT_LEADER;
+                    dstart = end_election(n);
+                } else if (n.role == RAFT_CANDIDATE) {                      // :220-221
+                    n.fl = (n.fl & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
+                    n.retry = 0;
+                    need_bo = true;
+                } else {
+                    dstart = end_election(n);
+                }
             }
         }
+        if (__ballot(need_bo)) {
+            const uint32_t w = quad_word(p, c, RAFT_RNG_BACKOFF);
+            if (need_bo) n.phase = scale_range(w, p.bmin, p.bmax);
+        }
+        start_sessions(p, c, n, dstart, cnt);
 
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
-        uint32_t todo = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) todo |= (g.fl[r] & FL_HB) ? (1u << r) : 0u;
-        while (__any(todo != 0)) {
-            if (todo != 0) {
+        uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
+        while (__ballot(todo != 0)) {
+            if (todo != 0) {                                                // group-uniform
                 const int s = __builtin_ctz(todo);
                 todo &= todo - 1u;
-                tick(g, p, c, s);
+                tick(p, c, n, s, cnt);
             }
         }
 
         // ---------------- C: client commands (S-11) ----------------
-        if (p.cmd_thr32 && (p.cmd_limit == 0 || g.cmdc < p.cmd_limit) && hw.y < p.cmd_thr32) {
-            bool any = false;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (g.role[r] == RAFT_LEADER && !(any && p.cmd_mode == RAFT_CMD_LOWEST_LEADER)) {
-                    append_command(g.rep(r), c.lg + r * c.cap, c.cap, hw.z, cnt);
-                    any = true;
-                }
+        if (p.cmd_thr32) {
+            const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
+            if ((p.cmd_limit == 0 || n.cmdc < p.cmd_limit) && hw1 < p.cmd_thr32 && lead) {
+                const bool tgt = p.cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
+                                                                      : ((lead >> r) & 1u) != 0;
+                if (tgt) append_command(n.rep(), c.lr, p.cap, hw2, cnt);
+                n.cmdc++;
             }
-            if (any) g.cmdc++;
         }
 
         // ---------------- K: end-of-step observations ----------------
-        int leaders = 0;
-        bool dual = false;
+        {
+            const bool isl = n.role == RAFT_LEADER;
+            const uint32_t lead = c.gbits(__ballot(isl));
+            if (isl) cnt.add(RAFT_C_LEADERS);
+            if (lead && r == __builtin_ctz(lead)) cnt.add(RAFT_C_GROUPS_WITH_LEADER);
+            if (__ballot(__popc(lead) >= 2)) {                              // rare
+                bool dual = false;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (g.role[r] != RAFT_LEADER) continue;
-            leaders++;
-#pragma unroll
-            for (int q = r + 1; q < R; ++q)
-                dual |= g.role[q] == RAFT_LEADER && g.term[q] == g.term[r];
-        }
-        cnt.add(RAFT_C_LEADERS, (uint32_t)leaders);
-        if (leaders > 0) cnt.add(RAFT_C_GROUPS_WITH_LEADER);
-        if (dual) cnt.add(RAFT_C_DUAL_LEADER_GROUPS);
-
-        resolve_timer_draws(g, p, c);
-    }
-
-    // the deferred ResettableCountdownTimer draws of this step (S-9)
-    __device__ __forceinline__ static void resolve_timer_draws(Group<R>& g, const DevParams& p, const Ctx& c) {
-#pragma unroll
-        for (int q = 0; q < (R + 3) / 4; ++q) {
-            bool need = false;
-#pragma unroll
-            for (int r = 4 * q; r < R && r < 4 * q + 4; ++r) need |= (g.fl[r] & FL_DRAW) != 0;
-            if (!__any(need)) continue;
-            if (need) {
-                const u32x4 w = draw(p, c.t, c.gid, RAFT_RNG_TIMER, (uint32_t)q);
-#pragma unroll
-                for (int r = 4 * q; r < R && r < 4 * q + 4; ++r) {
-                    if (g.fl[r] & FL_DRAW) {
-                        g.elec[r] = scale_range(word_of(w, r & 3), p.emin, p.emax);
-                        g.fl[r] &= ~FL_DRAW;
-                    }
+                for (int q = 0; q < R; ++q) {
+                    const int32_t tq = bcast(n.term, c.src(q));
+                    if (isl && r < q && ((lead >> q) & 1u) && tq == n.term) dual = true;
                 }
+                const uint32_t db = c.gbits(__ballot(dual));
+                if (db && r == 0) cnt.add(RAFT_C_DUAL_LEADER_GROUPS);
+            }
+        }
+
+        // the deferred ResettableCountdownTimer draws of this step (S-9)
+        if (__ballot((n.fl & FL_DRAW) != 0)) {
+            const uint32_t w = quad_word(p, c, RAFT_RNG_TIMER);
+            if (n.fl & FL_DRAW) {
+                n.elec = scale_range(w, p.emin, p.emax);
+                n.fl &= ~FL_DRAW;
             }
         }
     }
