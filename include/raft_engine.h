@@ -56,6 +56,7 @@ extern "C" {
 #define RAFT_LEADER    2
 
 #define RAFT_MAX_R 8
+#define RAFT_MAX_STEPS_PER_LAUNCH 256   /* steps fused into one kernel launch (LDS counter slots) */
 
 /* ---- command-injection modes (harness) ---------------- */
 #define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */
@@ -88,7 +89,7 @@ typedef struct raft_params {
     uint32_t cmd_ppm;           /* per group-step probability of one client command               */
     int32_t  cmd_mode;          /* RAFT_CMD_*                                                       */
     int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
-    int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch (0 = auto)         */
+    int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch, 0..RAFT_MAX_STEPS_PER_LAUNCH (0 = 1) */
     int32_t  reserved[7];
 } raft_params;
 
@@ -231,8 +232,10 @@ int raft_append_command_batch(raft_engine* e, const int64_t* group, const int32_
 /* ---- Philox4x32-10 (shared bit-for-bit with the CPU harness) -----------
  * Counter = (c0 = step, c1 = global group id, c2 = purpose, c3 = sub),
  * key = (seed lo32, seed hi32).  Purposes: */
-#define RAFT_RNG_TIMER        1u  /* sub = replica >> 2, word replica & 3: timeout   */
-#define RAFT_RNG_BACKOFF      2u  /* sub = replica >> 2, word replica & 3: backoff   */
+#define RAFT_RNG_TIMER        1u  /* sub = replica >> 2, word replica & 3: the replica's
+                                     per-step draw, scaled to the election timeout or to
+                                     the backoff (never both in one step)               */
+#define RAFT_RNG_BACKOFF      2u  /* reserved (the backoff shares the timer word)      */
 #define RAFT_RNG_VOTE_DROP    3u  /* sub = src | chunk << 8: 16-bit drop uniforms */
 #define RAFT_RNG_APPEND_DROP  4u  /* sub = src | chunk << 8                        */
 #define RAFT_RNG_HARNESS      5u  /* sub = 0: w0 churn, w1 command, w2 command id  */

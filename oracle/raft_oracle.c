@@ -422,7 +422,7 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
             end_election(&x, n);
         } else if (n->state == RAFT_CANDIDATE) {   /* :220-221 */
             n->backoff = 1;
-            n->phaseMs = draw_range(&x, t, RAFT_RNG_BACKOFF, r, p->backoff_min_ms, p->backoff_max_ms);
+            n->phaseMs = draw_range(&x, t, RAFT_RNG_TIMER, r, p->backoff_min_ms, p->backoff_max_ms);   /* S-9: the replica's timer word */
             n->retryMs = 0; n->votes = 0; n->latch = 0;
         } else {
             end_election(&x, n);

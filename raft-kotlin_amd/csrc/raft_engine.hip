@@ -141,15 +141,24 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 }
 
 // K lockstep steps of every group.  A wave holds GPW whole groups, one lane
-// per replica.  Counter partials are per wave and per step, packed 16-bit
-// pairs [k][NCW][nwaves]: no block barrier anywhere in the kernel.
+// per replica.  Counters: each wave reduces its lanes' packed 16-bit pairs
+// (DPP), adds them into the workgroup's LDS slot of the step, and the last
+// wave of the workgroup to finish the step writes the workgroup's partials
+// [k][NCW][nblocks].  One barrier (the LDS clear) per launch; waves of a
+// workgroup otherwise run free of each other.
+#ifndef RAFT_STEP_WAVES_PER_EU
+#define RAFT_STEP_WAVES_PER_EU 4
+#endif
 template <int R>
-__global__ __launch_bounds__(BLOCK) void step_kernel(DevParams p, uint32_t t0, int nsteps,
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
+void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
     using L = Lanes<R>;
+    extern __shared__ uint32_t lds_cnt[];                                 // [nsteps][NCW + 1]
+    for (int q = threadIdx.x; q < nsteps * (NCW + 1); q += BLOCK) lds_cnt[q] = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wid = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    const int nwaves = gridDim.x * WAVES_PER_BLOCK;
     const int j = lane / R;
     const int r = lane - j * R;
     const int64_t g = (int64_t)wid * L::GPW + j;
@@ -183,11 +192,17 @@ __global__ __launch_bounds__(BLOCK) void step_kernel(DevParams p, uint32_t t0, i
         Counters cnt;
         cnt.clear();
         Stepper<R>::step(p, c, n, cnt);
+        uint32_t* slot = lds_cnt + k * (NCW + 1);
 #pragma unroll
         for (int cw = 0; cw < NCW; ++cw) {
-            const uint32_t v = __ockl_wfred_add_u32(cnt.w[cw]);
-            if (lane == 0) partials[((int64_t)k * NCW + cw) * nwaves + wid] = v;
+            const uint32_t v = __ockl_wfred_add_u32(cnt.w[cw]);             // < 2^16 per half per wave
+            if (lane == 0 && v) atomicAdd(&slot[cw], v);                    // < 2^16 per half per block
         }
+        uint32_t arrived = 0;
+        if (lane == 0) arrived = atomicAdd(&slot[NCW], 1u);
+        arrived = __shfl(arrived, 0, 64);
+        if (arrived == WAVES_PER_BLOCK - 1 && lane < NCW)                  // last wave of the block
+            partials[((int64_t)k * NCW + lane) * gridDim.x + blockIdx.x] = slot[lane];
     }
     if (live) store_node(n, p, g, c.idx, r == 0);
 }
@@ -205,25 +220,26 @@ __global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
     p.st[fidx(p, F_T2, idx)] = (int32_t)b.x;
 }
 
-// counters[k][c] = sum over waves w of the 16-bit half (c & 1) of
-// partials[k][c >> 1][w]: one workgroup per (step, counter).
-__global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* __restrict__ partials, int nwaves,
+// counters[k][c] += sum over step workgroups b in this chunk of the 16-bit
+// half (c & 1) of partials[k][c >> 1][b]; grid (chunks, nsteps * NC), the
+// counters zeroed beforehand (int64 atomics: exact and order-independent).
+constexpr int REDUCE_CHUNK = 16 * BLOCK;
+__global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* __restrict__ partials, int nparts,
                                                                 int64_t* __restrict__ counters) {
-    __shared__ int64_t acc[WAVES_PER_BLOCK];
-    const int k = blockIdx.x / RAFT_COUNTER_STRIDE, c = blockIdx.x % RAFT_COUNTER_STRIDE;
-    uint32_t v = 0;                 // per-thread partial: < 2^16 * nwaves / BLOCK, fits
-    if (c < NC) {
-        const uint32_t* src = partials + ((int64_t)k * NCW + (c >> 1)) * nwaves;
-        const int sh = 16 * (c & 1);
-        for (int w = threadIdx.x; w < nwaves; w += BLOCK) v += (src[w] >> sh) & 0xFFFFu;
-    }
-    const uint32_t ws = __ockl_wfred_add_u32(v);   // < 2^32 for any G < 2^31 / 8 per step
+    __shared__ uint32_t acc[WAVES_PER_BLOCK];
+    const int k = blockIdx.y / NC, c = blockIdx.y % NC;
+    const uint32_t* src = partials + ((int64_t)k * NCW + (c >> 1)) * nparts;
+    const int sh = 16 * (c & 1);
+    const int b1 = min(nparts, (int)(blockIdx.x + 1) * REDUCE_CHUNK);
+    uint32_t v = 0;                 // < 2^16 * 16 per thread
+    for (int b = blockIdx.x * REDUCE_CHUNK + threadIdx.x; b < b1; b += BLOCK) v += (src[b] >> sh) & 0xFFFFu;
+    const uint32_t ws = __ockl_wfred_add_u32(v);   // < 2^16 * REDUCE_CHUNK = 2^28
     if ((threadIdx.x & 63) == 0) acc[threadIdx.x >> 6] = ws;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int64_t s = 0;
+        uint64_t s = 0;
         for (int w = 0; w < WAVES_PER_BLOCK; ++w) s += acc[w];
-        counters[(int64_t)k * RAFT_COUNTER_STRIDE + c] = s;
+        if (s) atomicAdd((unsigned long long*)&counters[(int64_t)k * RAFT_COUNTER_STRIDE + c], (unsigned long long)s);
     }
 }
 
@@ -422,7 +438,7 @@ struct raft_engine {
     uint64_t t;
     int K;                      // steps per launch
     int nblocks;                // step-kernel workgroups: ceil(G / (WAVES_PER_BLOCK * (64 / R)))
-    uint32_t* partials;         // [K][NCW][nwaves] packed per-wave counter partials
+    uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials
     int64_t* counters_dev;      // [K][STRIDE] scratch
     // step-kernel event timing
     bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
@@ -455,7 +471,7 @@ template <int R> struct InitL {
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
-        step_kernel<R><<<e->nblocks, BLOCK, 0, e->stream>>>(e->dp, t0, k, e->partials);
+        step_kernel<R><<<e->nblocks, BLOCK, (size_t)k * (NCW + 1) * 4, e->stream>>>(e->dp, t0, k, e->partials);
     }
 };
 template <int R> struct PackL {
@@ -515,6 +531,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     if (p->G < 1 || p->G > (int64_t)0x7FFFFFFF) return fail(RAFT_EINVAL, "G out of range");
     if (p->g0 < 0 || p->g0 + p->G > (int64_t)0x100000000ll) return fail(RAFT_EINVAL, "g0 + G exceeds 2^32");
     if (p->log_cap < 1) return fail(RAFT_EINVAL, "log_cap must be >= 1");
+    if (p->steps_per_launch < 0 || p->steps_per_launch > RAFT_MAX_STEPS_PER_LAUNCH)
+        return fail(RAFT_EINVAL, "steps_per_launch must be in 0..RAFT_MAX_STEPS_PER_LAUNCH");
     if (p->heartbeat_ms <= 0 || p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms)
         return fail(RAFT_EINVAL, "bad timer constants");
     int ndev = 0;
@@ -551,7 +569,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t gx_b = (size_t)GX_WORDS * G * 4;
     const size_t log_b = (size_t)G * R * p->log_cap * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t part_b = (size_t)e->K * NCW * e->nblocks * WAVES_PER_BLOCK * 4;
+    const size_t part_b = (size_t)e->K * NCW * e->nblocks * 4;
     const size_t cnt_b = (size_t)e->K * RAFT_COUNTER_STRIDE * 8;
     e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -619,7 +637,9 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
             e->ev_used += 2;
         }
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
-        reduce_counters_kernel<<<k * RAFT_COUNTER_STRIDE, BLOCK, 0, e->stream>>>(e->partials, e->nblocks * WAVES_PER_BLOCK, dst);
+        HIP_TRY(hipMemsetAsync(dst, 0, (size_t)k * RAFT_COUNTER_STRIDE * 8, e->stream));
+        const dim3 rg((unsigned)((e->nblocks + REDUCE_CHUNK - 1) / REDUCE_CHUNK), (unsigned)(k * NC));
+        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, dst);
         done += k;
     }
     HIP_TRY(hipGetLastError());

@@ -94,7 +94,11 @@ struct Counters {
 #pragma unroll
         for (int i = 0; i < NCW; ++i) w[i] = 0;
     }
+#ifdef RAFT_EXP_NO_COUNTERS
+    __device__ __forceinline__ void add(int, uint32_t = 1) {}
+#else
     __device__ __forceinline__ void add(int c, uint32_t v = 1) { w[c >> 1] += v << (16 * (c & 1)); }
+#endif
 };
 
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
@@ -246,8 +250,17 @@ struct Lanes {
     static constexpr int GPW = 64 / R;                 // groups per wave
     static constexpr uint32_t ALL = (1u << R) - 1u;
     static constexpr int MAJ = R / 2 + 1;              // RaftServer.kt:44
+    // Per-step Philox jobs (S-9), one per lane of the group, all evaluated in
+    // ONE Philox pass of the wave: J_HARNESS, then the NQ timer quads (the
+    // per-replica draw word, used by the election timer and the backoff), then
+    // the NCH drop-word chunks of the first leader to tick and of the first
+    // RequestVote sender.  Jobs that do not fit in R lanes are drawn on demand.
     static constexpr int NQ = (R + 3) / 4;             // Philox calls per 4-replica quad
-    static constexpr bool JOBS = 1 + 2 * NQ <= R;      // per-step draws fit one lane each
+    static constexpr int NCH = (R + 2) / 4;            // drop-word chunks per sender: ceil((R - 1) / 4)
+    static constexpr int J_TIMER = 1, J_TICK = 1 + NQ, J_VOTE = 1 + NQ + NCH;
+    static constexpr bool JOBS = 1 + NQ <= R;          // harness + timer quads fit
+    static constexpr bool TICK_JOB = JOBS && J_TICK + NCH <= R;
+    static constexpr bool VOTE_JOB = JOBS && J_VOTE + NCH <= R;
 
     // lanes whose replica index is s (compile-time masks)
     static constexpr uint64_t lanes_of(int s) {
@@ -268,6 +281,7 @@ struct Ctx {
     uint32_t part;            // replicas on side B of this step's partition
     uint2* lr;                // this replica's log
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS)
+    int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
 
     __device__ __forceinline__ uint32_t gbits(uint64_t b) const {
         return (uint32_t)(b >> base) & Lanes<R>::ALL;
@@ -286,32 +300,57 @@ __device__ __forceinline__ bool lost(const DevParams& p, const Ctx<R>& c, int s,
 
 // 16-bit drop uniforms of sender s for this lane as destination d (S-9):
 // word dd = (d < s ? d : d - 1) of Philox(t, gid, purpose, s | (dd >> 2) << 8).
-// Every lane of the group evaluates it for its own dd, so one Philox
-// evaluation of the wave serves every destination.
+// drop_word_direct evaluates it in this lane (one Philox pass serves every
+// destination of the wave); drop_word takes it from the step's jobs when they
+// hold sender s (first_job = J_TICK / J_VOTE), else draws it directly.
+// drop_word MUST be called in group-uniform control flow.
 template <int R>
-__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s) {
-    if (p.drop_thr16 == 0) return 0u;
+__device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s) {
+#ifdef RAFT_EXP_CHEAP_DROP
+    return (c.gid * 0x9E3779B1u) ^ (c.t * 0x85EBCA6Bu) ^ ((uint32_t)s << 13) ^ ((uint32_t)c.r << 7);
+#endif
     const int dd = c.r < s ? c.r : c.r - 1;
     const int q = dd < 0 ? 0 : dd;
     const u32x4 w = draw(p, c.t, c.gid, purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
     return word_of(w, q & 3);
 }
 
-// The step's per-(group, replica) timer / backoff draw word for this lane,
-// word r & 3 of Philox(t, gid, purpose, r >> 2).  With JOBS the group's lanes
-// computed them at step start: lane 1 + q holds timer quad q, lane 1 + NQ + q
-// backoff quad q.  MUST be called in group-uniform control flow.
 template <int R>
-__device__ __forceinline__ uint32_t quad_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose) {
+__device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int k) {
+    const int sl = c.src(job_lane);
+    const uint32_t a = bcastu(c.job.x, sl), b = bcastu(c.job.y, sl);
+    const uint32_t x = bcastu(c.job.z, sl), y = bcastu(c.job.w, sl);
+    return k == 0 ? a : k == 1 ? b : k == 2 ? x : y;
+}
+
+template <int R, bool HAVE_JOB>
+__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s,
+                                              int first_job, int s_job) {
+    if (p.drop_thr16 == 0) return 0u;
+    uint32_t w = 0;
+    bool need = true;
+    if constexpr (HAVE_JOB) {
+        const int dd = c.r < s ? c.r : c.r - 1;
+        const int q = dd < 0 ? 0 : dd;
+        w = job_word(c, first_job + (q >> 2), q & 3);
+        need = s != s_job;
+    }
+    if (__ballot(need)) {
+        if (need) w = drop_word_direct(p, c, purpose, s);
+    }
+    return w;
+}
+
+// The step's per-replica draw word, word r & 3 of Philox(t, gid, TIMER, r >> 2)
+// (S-9): the election timeout and the candidate backoff both scale it (a
+// replica never needs both in one step).  MUST be called in group-uniform
+// control flow.
+template <int R>
+__device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>& c) {
     if constexpr (Lanes<R>::JOBS) {
-        const int first = purpose == RAFT_RNG_TIMER ? 1 : 1 + Lanes<R>::NQ;
-        const int sl = c.src(first + (c.r >> 2));
-        const uint32_t a = bcastu(c.job.x, sl), b = bcastu(c.job.y, sl);
-        const uint32_t x = bcastu(c.job.z, sl), y = bcastu(c.job.w, sl);
-        const int k = c.r & 3;
-        return k == 0 ? a : k == 1 ? b : k == 2 ? x : y;
+        return job_word(c, Lanes<R>::J_TIMER + (c.r >> 2), c.r & 3);
     } else {
-        return word_of(draw(p, c.t, c.gid, purpose, (uint32_t)(c.r >> 2)), c.r & 3);
+        return word_of(draw(p, c.t, c.gid, RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
     }
 }
 
@@ -441,7 +480,7 @@ struct Stepper {
         if (ld2) lent = ls[i - 1];
         if (ld3) dpt = (int32_t)c.lr[prev].x;
 
-        const uint32_t dw = drop_word(p, c, RAFT_RNG_APPEND_DROP, s);
+        const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, s, L::J_TICK, c.s_tick);
         bool lreq = false, lresp = false, delivered = false, succ = false;
         int32_t rterm = 0;
         if (ok) {
@@ -513,34 +552,10 @@ struct Stepper {
     // Called by all 64 lanes (converged); `n` of a dead lane is inert.
     __device__ __forceinline__ static void step(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt) {
         const int r = c.r;
-        // ---------------- per-step Philox jobs (S-9) ----------------
-        // lane 0 of a group: harness; lanes 1..NQ: timer quads; lanes
-        // NQ+1..2NQ: backoff quads.  One Philox evaluation of the wave.
-        uint32_t hw0, hw1, hw2;
-        if constexpr (L::JOBS) {
-            const uint32_t purpose = r == 0 ? RAFT_RNG_HARNESS : r <= L::NQ ? RAFT_RNG_TIMER : RAFT_RNG_BACKOFF;
-            const uint32_t sub = r == 0 ? 0u : r <= L::NQ ? (uint32_t)(r - 1) : (uint32_t)(r - 1 - L::NQ);
-            c.job = draw(p, c.t, c.gid, purpose, sub);
-            hw0 = bcastu(c.job.x, c.base);
-            hw1 = bcastu(c.job.y, c.base);
-            hw2 = bcastu(c.job.z, c.base);
-        } else {
-            const u32x4 h = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
-            hw0 = h.x; hw1 = h.y; hw2 = h.z;
-        }
-
-        // ---------------- H: harness ----------------
-        {
-            int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
-            if (rem > 0) { rem--; if (rem == 0) rep = 0; }
-            const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
-            if (p.churn_thr32 && p.churn_steps > 0 && rem == 0 && hw0 < p.churn_thr32 && lead) {
-                rep = __builtin_ctz(lead);                                  // lowest-id LEADER
-                rem = p.churn_steps;
-            }
-            n.iso = rem > 0 ? (rem << 8) | rep : 0;
-            c.iso = rem > 0 ? rep : -1;
-        }
+        // H needs the roles at step start (the lowest-id LEADER to isolate);
+        // T draws no randomness, so it runs before the step's Philox pass and
+        // that pass already knows the first RequestVote sender.
+        const uint32_t lead0 = c.gbits(__ballot(n.role == RAFT_LEADER));
 
         // ---------------- T: timers and election clocks ----------------
         uint32_t send = 0;
@@ -581,20 +596,69 @@ struct Stepper {
         }
         start_sessions(p, c, n, sstart, cnt);
 
+        // ---------------- the step's Philox pass (S-9) ----------------
+        // lane J_HARNESS of a group: harness words; lanes J_TIMER..: timer
+        // quads; lanes J_TICK.. / J_VOTE..: drop-word chunks of the first
+        // leader to tick (lowest heartbeat session now) and of the first
+        // RequestVote sender.  One Philox evaluation of the wave.
+        uint32_t hw0, hw1, hw2;
+        {
+            const uint32_t hb = c.gbits(__ballot((n.fl & FL_HB) != 0));
+            const uint32_t sd = c.gbits(__ballot(send != 0));
+            c.s_tick = hb ? __builtin_ctz(hb) : -1;
+            c.s_vote = sd ? __builtin_ctz(sd) : -1;
+        }
+        if constexpr (L::JOBS) {
+            uint32_t purpose = RAFT_RNG_HARNESS, sub = 0;
+            if (r >= L::J_TIMER && r < L::J_TICK) {
+                purpose = RAFT_RNG_TIMER; sub = (uint32_t)(r - L::J_TIMER);
+            } else if (r >= L::J_TICK && r < L::J_VOTE) {
+                purpose = RAFT_RNG_APPEND_DROP; sub = (uint32_t)(c.s_tick & 0xFF) | ((uint32_t)(r - L::J_TICK) << 8);
+            } else if (r >= L::J_VOTE) {
+                purpose = RAFT_RNG_VOTE_DROP; sub = (uint32_t)(c.s_vote & 0xFF) | ((uint32_t)(r - L::J_VOTE) << 8);
+            }
+#ifdef RAFT_EXP_CHEAP_JOB
+            c.job = u32x4{c.gid * 0x9E3779B1u ^ c.t, c.t * 0x85EBCA6Bu ^ sub, purpose ^ c.gid, c.gid + c.t};
+#else
+            c.job = draw(p, c.t, c.gid, purpose, sub);
+#endif
+            hw0 = bcastu(c.job.x, c.base);
+            hw1 = bcastu(c.job.y, c.base);
+            hw2 = bcastu(c.job.z, c.base);
+        } else {
+            const u32x4 h = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
+            hw0 = h.x; hw1 = h.y; hw2 = h.z;
+        }
+
+        // ---------------- H: harness ----------------
+        {
+            int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
+            if (rem > 0) { rem--; if (rem == 0) rep = 0; }
+            if (p.churn_thr32 && p.churn_steps > 0 && rem == 0 && hw0 < p.churn_thr32 && lead0) {
+                rep = __builtin_ctz(lead0);                                 // lowest-id LEADER
+                rem = p.churn_steps;
+            }
+            n.iso = rem > 0 ? (rem << 8) | rep : 0;
+            c.iso = rem > 0 ? rep : -1;
+        }
+
         // ---------------- V: RequestVote fan-out (S-3) ----------------
-        const uint64_t sendb = __ballot(send != 0);
-        if (sendb) {
-#pragma unroll
-            for (int s = 0; s < R; ++s) {
-                if (!(sendb & L::lanes_of(s))) continue;                    // wave-uniform
+        // Each group walks its own senders in ascending order (group-uniform,
+        // runtime s), so the wave runs as many rounds as its busiest group has
+        // senders -- usually one -- with one handler per destination lane.
+        uint32_t vtodo = c.gbits(__ballot(send != 0));
+        while (__ballot(vtodo != 0)) {
+            if (vtodo != 0) {                                               // group-uniform
+                const int s = __builtin_ctz(vtodo);
+                vtodo &= vtodo - 1u;
                 const int sl = c.src(s);
                 const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
                 const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
                 const int32_t st = bcast(n.term, sl);
-                const uint32_t dw = drop_word(p, c, RAFT_RNG_VOTE_DROP, s);
+                const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, L::J_VOTE, c.s_vote);
                 bool lreq = false, lresp = false, delivered = false, granted = false;
                 int32_t rterm = 0;
-                if (c.live && ((ms >> r) & 1u)) {
+                if ((ms >> r) & 1u) {
                     lreq = lost(p, c, s, r, dw, 0);                         // retry{} swallows, Commons.kt:41
                     if (!lreq) {
                         vote_handler(n.rep(), rt, s + 1, rli, rlt, cnt, rterm, granted);
@@ -607,7 +671,7 @@ struct Stepper {
                 const uint32_t dl = c.gbits(__ballot(delivered));
                 const uint32_t gr = c.gbits(__ballot(delivered && granted));
                 const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
-                if (r == s && ms) {
+                if (r == s) {
                     uint32_t f = n.fl & ~(dl << PEND_SH);
                     f += (uint32_t)__popc(dl) << LATCH_SH;                  // :209 countDown()
                     f += (uint32_t)__popc(gr) << VOTES_SH;                  // :211
@@ -638,7 +702,7 @@ struct Stepper {
             }
         }
         if (__ballot(need_bo)) {
-            const uint32_t w = quad_word(p, c, RAFT_RNG_BACKOFF);
+            const uint32_t w = timer_word(p, c);
             if (need_bo) n.phase = scale_range(w, p.bmin, p.bmax);
         }
         start_sessions(p, c, n, dstart, cnt);
@@ -684,7 +748,7 @@ struct Stepper {
 
         // the deferred ResettableCountdownTimer draws of this step (S-9)
         if (__ballot((n.fl & FL_DRAW) != 0)) {
-            const uint32_t w = quad_word(p, c, RAFT_RNG_TIMER);
+            const uint32_t w = timer_word(p, c);
             if (n.fl & FL_DRAW) {
                 n.elec = scale_range(w, p.emin, p.emax);
                 n.fl &= ~FL_DRAW;
