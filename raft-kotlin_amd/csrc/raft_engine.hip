@@ -194,9 +194,8 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         Stepper<R>::step(p, c, n, cnt);
         uint32_t* slot = lds_cnt + k * (NCW + 1);
 #pragma unroll
-        for (int cw = 0; cw < NCW; ++cw) {
-            const uint32_t v = __ockl_wfred_add_u32(cnt.w[cw]);             // < 2^16 per half per wave
-            if (lane == 0 && v) atomicAdd(&slot[cw], v);                    // < 2^16 per half per block
+        for (int cw = 0; cw < NCW; ++cw) {                                  // wave totals (SGPRs)
+            if (lane == 0 && cnt.s[cw]) atomicAdd(&slot[cw], cnt.s[cw]);    // < 2^16 per half per block
         }
         uint32_t arrived = 0;
         if (lane == 0) arrived = atomicAdd(&slot[NCW], 1u);

@@ -86,19 +86,36 @@ struct DevParams {
 
 struct Entry { int32_t term; uint32_t cmd; };
 
-// Per-lane step counters, two 16-bit counters per register (a lane's count in
-// one step is < 2^16 / 64, so a wave sum of a packed word cannot carry).
+// Step counters.  A handler marks an event in its lane's bit mask `ev` (bit
+// c = counter c; every counter fires at most once per lane between two
+// flushes).  flush<MASK>() -- called at wave-uniform points -- adds
+// popcount(ballot(bit c)) into the wave-uniform (SGPR) totals `s`, two 16-bit
+// counters per word (a wave's count per step is < 2^16), and clears `ev`.
+#define CBIT(c) (1u << (c))
 struct Counters {
-    uint32_t w[NCW];
+    uint32_t ev;
+    uint32_t s[NCW];
     __device__ __forceinline__ void clear() {
+        ev = 0;
 #pragma unroll
-        for (int i = 0; i < NCW; ++i) w[i] = 0;
+        for (int i = 0; i < NCW; ++i) s[i] = 0;
     }
 #ifdef RAFT_EXP_NO_COUNTERS
-    __device__ __forceinline__ void add(int, uint32_t = 1) {}
+    __device__ __forceinline__ void add(int) {}
 #else
-    __device__ __forceinline__ void add(int c, uint32_t v = 1) { w[c >> 1] += v << (16 * (c & 1)); }
+    __device__ __forceinline__ void add(int c) { ev |= 1u << c; }
 #endif
+    template <uint32_t MASK>
+    __device__ __forceinline__ void flush() {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if ((MASK >> c) & 1u) {
+                const uint32_t k = (uint32_t)__popcll(__ballot((ev >> c) & 1u));
+                s[c >> 1] += k << (16 * (c & 1));
+            }
+        }
+        ev = 0;
+    }
 };
 
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
@@ -357,6 +374,19 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
 template <int R>
 struct Stepper {
     using L = Lanes<R>;
+    static constexpr uint32_t M_T = CBIT(RAFT_C_TIMEOUTS) | CBIT(RAFT_C_ROUNDS) | CBIT(RAFT_C_VOTE_LOG_READS) |
+                                    CBIT(RAFT_C_LEADERS_ELECTED);
+    static constexpr uint32_t M_V = CBIT(RAFT_C_MSG_DROPPED) | CBIT(RAFT_C_VOTE_LOG_READS) | CBIT(RAFT_C_VOTES_GRANTED);
+    static constexpr uint32_t M_D = CBIT(RAFT_C_LEADERS_ELECTED);
+    static constexpr uint32_t M_A = CBIT(RAFT_C_SESSIONS_TICKED) | CBIT(RAFT_C_PREV_READS_LEADER) |
+                                    CBIT(RAFT_C_ENTRY_READS_LEADER) | CBIT(RAFT_C_APPEND_SKIPPED) |
+                                    CBIT(RAFT_C_APPEND_SENT) | CBIT(RAFT_C_MSG_DROPPED) |
+                                    CBIT(RAFT_C_COMMIT_REGRESSIONS) | CBIT(RAFT_C_PREV_READS_FOLLOWER) |
+                                    CBIT(RAFT_C_ENTRY_WRITES) | CBIT(RAFT_C_LOG_OVERFLOW) |
+                                    CBIT(RAFT_C_ENTRIES_ACKED) | CBIT(RAFT_C_COMMITS);
+    static constexpr uint32_t M_C = CBIT(RAFT_C_COMMANDS) | CBIT(RAFT_C_LOG_OVERFLOW);
+    static constexpr uint32_t M_K = CBIT(RAFT_C_LEADERS) | CBIT(RAFT_C_GROUPS_WITH_LEADER) |
+                                    CBIT(RAFT_C_DUAL_LEADER_GROUPS);
     static constexpr int MAJ = L::MAJ;
     static constexpr uint32_t ALL = L::ALL;
 
@@ -548,6 +578,45 @@ struct Stepper {
         }
     }
 
+    // One RequestVote round: every group with a pending sender delivers the
+    // requests of its lowest remaining sender s to all destinations at once
+    // (group-uniform control flow).
+    __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
+                                                      uint32_t& vtodo, uint32_t send, int32_t qt, int32_t qli,
+                                                      int32_t qlt) {
+        const int r = c.r;
+        const int s = __builtin_ctz(vtodo);
+        vtodo &= vtodo - 1u;
+        const int sl = c.src(s);
+        const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
+        const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
+        const int32_t st = bcast(n.term, sl);
+        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, L::J_VOTE, c.s_vote);
+        bool lreq = false, lresp = false, delivered = false, granted = false;
+        int32_t rterm = 0;
+        if ((ms >> r) & 1u) {
+            lreq = lost(p, c, s, r, dw, 0);                         // retry{} swallows, Commons.kt:41
+            if (!lreq) {
+                vote_handler(n.rep(), rt, s + 1, rli, rlt, cnt, rterm, granted);
+                lresp = lost(p, c, s, r, dw, 1);
+                delivered = !lresp;
+            }
+        }
+        if (lreq | lresp) cnt.add(RAFT_C_MSG_DROPPED);
+        // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
+        const uint32_t dl = c.gbits(__ballot(delivered));
+        const uint32_t gr = c.gbits(__ballot(delivered && granted));
+        const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
+        if (r == s) {
+            uint32_t f = n.fl & ~(dl << PEND_SH);
+            f += (uint32_t)__popc(dl) << LATCH_SH;                  // :209 countDown()
+            f += (uint32_t)__popc(gr) << VOTES_SH;                  // :211
+            n.fl = f;
+            if (hi) n.role = RAFT_FOLLOWER;                         // :210 (Q6)
+            if ((f >> PEND_SH) & 0xFFu) n.retry = p.retry;
+        }
+    }
+
     // One lockstep step of every group of the wave.
     // Called by all 64 lanes (converged); `n` of a dead lane is inert.
     __device__ __forceinline__ static void step(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt) {
@@ -595,6 +664,7 @@ struct Stepper {
             }
         }
         start_sessions(p, c, n, sstart, cnt);
+        cnt.flush<M_T>();
 
         // ---------------- the step's Philox pass (S-9) ----------------
         // lane J_HARNESS of a group: harness words; lanes J_TIMER..: timer
@@ -630,6 +700,12 @@ struct Stepper {
             hw0 = h.x; hw1 = h.y; hw2 = h.z;
         }
 
+#ifdef RAFT_EXP_EXTRA_PHILOX
+        {   // timing experiment only: one more Philox pass of the wave
+            const u32x4 x = draw(p, c.t ^ 0x5A5A5A5Au, c.gid, 77u, (uint32_t)r);
+            if (x.x == 0x12345678u && x.y == 0x9ABCDEF0u && x.z == 1u) cnt.add(RAFT_C_LEADERS);
+        }
+#endif
         // ---------------- H: harness ----------------
         {
             int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
@@ -647,38 +723,12 @@ struct Stepper {
         // runtime s), so the wave runs as many rounds as its busiest group has
         // senders -- usually one -- with one handler per destination lane.
         uint32_t vtodo = c.gbits(__ballot(send != 0));
-        while (__ballot(vtodo != 0)) {
-            if (vtodo != 0) {                                               // group-uniform
-                const int s = __builtin_ctz(vtodo);
-                vtodo &= vtodo - 1u;
-                const int sl = c.src(s);
-                const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
-                const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
-                const int32_t st = bcast(n.term, sl);
-                const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, L::J_VOTE, c.s_vote);
-                bool lreq = false, lresp = false, delivered = false, granted = false;
-                int32_t rterm = 0;
-                if ((ms >> r) & 1u) {
-                    lreq = lost(p, c, s, r, dw, 0);                         // retry{} swallows, Commons.kt:41
-                    if (!lreq) {
-                        vote_handler(n.rep(), rt, s + 1, rli, rlt, cnt, rterm, granted);
-                        lresp = lost(p, c, s, r, dw, 1);
-                        delivered = !lresp;
-                    }
-                }
-                if (lreq | lresp) cnt.add(RAFT_C_MSG_DROPPED);
-                // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
-                const uint32_t dl = c.gbits(__ballot(delivered));
-                const uint32_t gr = c.gbits(__ballot(delivered && granted));
-                const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
-                if (r == s) {
-                    uint32_t f = n.fl & ~(dl << PEND_SH);
-                    f += (uint32_t)__popc(dl) << LATCH_SH;                  // :209 countDown()
-                    f += (uint32_t)__popc(gr) << VOTES_SH;                  // :211
-                    n.fl = f;
-                    if (hi) n.role = RAFT_FOLLOWER;                         // :210 (Q6)
-                    if ((f >> PEND_SH) & 0xFFu) n.retry = p.retry;
-                }
+        if (__ballot(vtodo != 0)) {
+            if (vtodo != 0) vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);   // group-uniform
+            cnt.flush<M_V>();
+            while (__ballot(vtodo != 0)) {                                  // groups with 2+ senders (rare)
+                if (vtodo != 0) vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                cnt.flush<M_V>();
             }
         }
 
@@ -706,15 +756,23 @@ struct Stepper {
             if (need_bo) n.phase = scale_range(w, p.bmin, p.bmax);
         }
         start_sessions(p, c, n, dstart, cnt);
+        cnt.flush<M_D>();
 
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
         uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
-        while (__ballot(todo != 0)) {
-            if (todo != 0) {                                                // group-uniform
+        if (todo != 0) {                                                    // group-uniform
+            const int s = __builtin_ctz(todo);
+            todo &= todo - 1u;
+            tick(p, c, n, s, cnt);
+        }
+        cnt.flush<M_A>();
+        while (__ballot(todo != 0)) {                                       // 2+ sessions (rare)
+            if (todo != 0) {
                 const int s = __builtin_ctz(todo);
                 todo &= todo - 1u;
                 tick(p, c, n, s, cnt);
             }
+            cnt.flush<M_A>();
         }
 
         // ---------------- C: client commands (S-11) ----------------
@@ -726,6 +784,7 @@ struct Stepper {
                 if (tgt) append_command(n.rep(), c.lr, p.cap, hw2, cnt);
                 n.cmdc++;
             }
+            cnt.flush<M_C>();
         }
 
         // ---------------- K: end-of-step observations ----------------
@@ -744,6 +803,7 @@ struct Stepper {
                 const uint32_t db = c.gbits(__ballot(dual));
                 if (db && r == 0) cnt.add(RAFT_C_DUAL_LEADER_GROUPS);
             }
+            cnt.flush<M_K>();
         }
 
         // the deferred ResettableCountdownTimer draws of this step (S-9)
