@@ -201,6 +201,9 @@ void*   raft_engine_stream(raft_engine* e);
 int raft_engine_set_kernel_timing(raft_engine* e, int enable);
 int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches);
 int64_t raft_engine_step_index(raft_engine* e);   /* steps executed so far */
+/* Steps fused into one kernel launch from now on (0 = 1), at most
+ * RAFT_MAX_STEPS_PER_LAUNCH.  Results do not depend on it. */
+int     raft_engine_set_steps_per_launch(raft_engine* e, int32_t k);
 /* Set the index of the next step (its Philox counter c0); with write_state
  * this resumes a run exported at any step. */
 int     raft_engine_set_step_index(raft_engine* e, int64_t t);

@@ -39,6 +39,7 @@ COUNTER_NAMES = [
 ]
 NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
+MAX_STEPS_PER_LAUNCH = 256
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
 
 FIELD_NAMES = ["term", "voted", "role", "commit", "last", "phys",
@@ -170,6 +171,7 @@ def load_library(path: str | None = None):
         "raft_engine_kernel_time": (C.c_int, [eng, P(C.c_double), P(I64)]),
         "raft_engine_step_index": (I64, [eng]),
         "raft_engine_set_step_index": (C.c_int, [eng, I64]),
+        "raft_engine_set_steps_per_launch": (C.c_int, [eng, I32]),
         "raft_engine_device_bytes": (I64, [eng]),
         "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
         "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
@@ -194,7 +196,8 @@ EXPORTED_SYMBOLS = [
     "raft_params_default", "raft_last_error", "raft_abi_version", "raft_engine_create",
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
-    "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_device_bytes",
+    "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
+    "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_philox4x32_10",

@@ -23,6 +23,12 @@ RAFT_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
 
 RAFT_HD u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                            uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Keep the round keys local to this call: without the barrier the
+    // optimiser hoists all 20 (uniform) round keys out of the step loop and
+    // they pin 20 SGPRs for the whole kernel (spilled to VGPR lanes).
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         // one full 32x32->64 product per multiplier (a single v_mad_u64_u32 on gfx950)

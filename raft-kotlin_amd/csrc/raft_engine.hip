@@ -181,6 +181,11 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;
         c.t = t;
+        // Rematerialise the lane geometry every step: otherwise the optimiser
+        // hoists dozens of loop-invariant lane masks (r == 1, r < 2, ...) out
+        // of the step loop, and each one pins an SGPR pair for the whole
+        // kernel (spilled to VGPR lanes and reloaded at every use).
+        asm volatile("" : "+v"(c.r), "+v"(c.base));
         if (p.part_period > 0) {                                          // S-11 partitions
             const uint32_t ph = t % (uint32_t)p.part_period;
             if ((int64_t)ph < p.part_len) {
@@ -568,8 +573,9 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t gx_b = (size_t)GX_WORDS * G * 4;
     const size_t log_b = (size_t)G * R * p->log_cap * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t part_b = (size_t)e->K * NCW * e->nblocks * 4;
-    const size_t cnt_b = (size_t)e->K * RAFT_COUNTER_STRIDE * 8;
+    // sized for the largest launch, so steps_per_launch can change later
+    const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;
+    const size_t cnt_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * RAFT_COUNTER_STRIDE * 8;
     e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (err != hipSuccess) { delete e; return fail(RAFT_EDEVICE, "hipStreamCreate failed"); }
@@ -692,6 +698,12 @@ int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches)
     return RAFT_OK;
 }
 int64_t raft_engine_step_index(raft_engine* e) { return e ? (int64_t)e->t : -1; }
+int raft_engine_set_steps_per_launch(raft_engine* e, int32_t k) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (k < 0 || k > RAFT_MAX_STEPS_PER_LAUNCH) return fail(RAFT_EINVAL, "steps_per_launch out of range");
+    e->K = k > 0 ? k : 1;
+    return RAFT_OK;
+}
 int raft_engine_set_step_index(raft_engine* e, int64_t t) {
     if (!e || t < 0 || t > (int64_t)0xFFFFFFFFll) return fail(RAFT_EINVAL, "bad step index");
     e->t = (uint64_t)t;

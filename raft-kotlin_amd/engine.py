@@ -73,6 +73,10 @@ class RaftEngine:
     def step_index(self, t: int):
         self._check(self._lib.raft_engine_set_step_index(self._h, int(t)), "set_step_index")
 
+    def set_steps_per_launch(self, k: int):
+        """Steps fused into one kernel launch from now on (results do not depend on it)."""
+        self._check(self._lib.raft_engine_set_steps_per_launch(self._h, int(k)), "set_steps_per_launch")
+
     @property
     def device_bytes(self) -> int:
         return int(self._lib.raft_engine_device_bytes(self._h))
