@@ -34,23 +34,37 @@ abi = importlib.import_module("raft-kotlin_amd.abi")
 
 METRIC = "Raft group-steps/sec (whole node) at 1M×5-replica groups; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-STATE_BYTES_PER_REPLICA = 4 * (abi.NUM_FIELDS + 3)   # 10 canonical fields + the log-tail cache (t1, t2, c1)
-GROUP_EXTRA_BYTES = 4 * abi.GROUP_EXTRA
+# per replica: 10 canonical fields + the log-tail cache (t1, t2, c1) + the
+# primary-session column (nextIndex, matchIndex); per group: 3 harness words
+REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
+GROUP_BYTES = 4 * 3
 
 
 def algorithmic_bytes(c: np.ndarray, G: int, R: int, launches: int) -> float:
-    """Algorithmic HBM bytes of the step kernel over the counted steps
-    (DESIGN.md §4): the group state is read and written once per launch, an
-    active leader session (2R int32) once per launch, and every log slot the
-    handlers touch once (4 B per term read, 8 B per entry read/write)."""
+    """Algorithmic HBM bytes of `launches` step-kernel launches over the
+    counted steps, a LOWER bound: the group state is read and
+    written once per launch and every log entry a handler or appendCommand
+    stores is written (8 B).  Log reads are not counted: the register-resident
+    tail cache answers the steady-state ones, and the rest are rare."""
     ix = abi.C_INDEX
-    state = 2.0 * G * (R * STATE_BYTES_PER_REPLICA + GROUP_EXTRA_BYTES) * launches
-    steps = max(1, c.shape[0])
-    sessions = 2.0 * 8 * R * (c[:, ix["sessions_ticked"]].sum() / steps) * launches
-    log = (4.0 * c[:, ix["prev_reads_leader"]].sum() + 8.0 * c[:, ix["entry_reads_leader"]].sum()
-           + 4.0 * c[:, ix["prev_reads_follower"]].sum() + 8.0 * c[:, ix["entry_writes"]].sum()
-           + 4.0 * c[:, ix["vote_log_reads"]].sum() + 8.0 * c[:, ix["commands"]].sum())
-    return state + sessions + log
+    state = 2.0 * G * (R * REPLICA_BYTES + GROUP_BYTES) * launches
+    log = 8.0 * (c[:, ix["entry_writes"]].sum() + c[:, ix["commands"]].sum())
+    return state + log
+
+
+def load_traffic(workload: dict):
+    """HBM traffic per launch measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    for this exact workload (scripts/traffic.sh -> profiles/traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for row in rows:
+        if all(row.get(k) == v for k, v in workload.items()):
+            return row
+    return None
 
 
 def cpu_baseline(args, kw, log_cap):
@@ -83,7 +97,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
-    ap.add_argument("--steps-per-launch", type=int, default=0)
+    ap.add_argument("--steps-per-launch", type=int, default=64,
+                    help="lockstep steps fused into one kernel launch (state stays in VGPRs)")
+    ap.add_argument("--stream-steps", type=int, default=200,
+                    help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
     ap.add_argument("--reduce-every", type=int, default=256, help="steps per counter all-reduce")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
@@ -115,7 +132,7 @@ def main():
     else:
         G_local = args.groups // world + (1 if rank < args.groups % world else 0)
         g0 = rank * (args.groups // world) + min(rank, args.groups % world)
-    total_steps = args.warmup + args.steps
+    total_steps = args.warmup + args.steps + args.stream_steps
     log_cap = args.log_cap or int(64 + 0.3 * total_steps)
     spl = args.steps_per_launch
     params = abi.make_params(log_cap=log_cap, steps_per_launch=spl, **dict(kw, G=G_local, g0=g0))
@@ -186,6 +203,30 @@ def main():
     kern_avg_ms = kern_ms / max(1, launches)
     achieved = bytes_alg / launches / (kern_avg_ms / 1e3) / 1e9 if launches else 0.0
     overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
+    K = spl or 1
+    tr = load_traffic({"config": args.config, "groups": G_local, "steps_per_launch": K})
+
+    # ---- streaming leg (untimed for `value`): one step per launch, so every
+    # launch streams the whole group state HBM -> VGPRs -> HBM.  Its roofline
+    # is the HBM-bound formulation of the same step. ----
+    stream = None
+    if args.stream_steps > 0:
+        eng.set_steps_per_launch(1)
+        sc = torch.zeros((args.stream_steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+        eng.set_kernel_timing(True)
+        eng.step_async(args.stream_steps, sc.data_ptr())
+        eng.sync()
+        s_ms, s_n = eng.kernel_time()
+        eng.set_kernel_timing(False)
+        cs = sc.cpu().numpy()[:, : abi.NUM_COUNTERS]
+        s_avg = s_ms / max(1, s_n)
+        s_bytes = algorithmic_bytes(cs, G_local, R, s_n) / max(1, s_n)
+        s_ach = s_bytes / (s_avg / 1e3) / 1e9
+        s_tr = load_traffic({"config": args.config, "groups": G_local, "steps_per_launch": 1})
+        stream = {"steps_per_launch": 1, "steps": args.stream_steps, "kernel_avg_ms": s_avg,
+                  "alg_bytes_per_launch": s_bytes, "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": s_ach / HBM_PEAK_GBS, "traffic": s_tr["bytes_per_launch"] if s_tr else None,
+                  "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
     out = {
         "metric": METRIC,
@@ -205,15 +246,20 @@ def main():
                         + (", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step"
                            if args.config == 3 else ""),
             "groups_total": total_groups, "replicas": R, "log_cap": log_cap,
-            "steps_per_launch": spl or 1, "parallelism": f"shard-by-group x{world}",
+            "steps_per_launch": K, "parallelism": f"shard-by-group x{world}",
             "counter_allreduce_every": args.reduce_every if world > 1 else None,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "step_kernel", "kernel_avg_ms": kern_avg_ms, "launches": launches,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
+            "kernel": f"step_kernel<{R}> x{K} fused steps", "kernel_avg_ms": kern_avg_ms, "launches": launches,
             "alg_bytes_per_launch": bytes_alg / max(1, launches),
+            "traffic_source": tr["source"] if tr else None,
+            "note": "fused launches keep every replica in VGPRs for K steps, so HBM carries the state "
+                    "once per K steps and the kernel is VALU-issue bound; roofline_streaming is the "
+                    "same step at one step per launch (HBM-bound formulation)",
         },
+        "roofline_streaming": stream,
         "valid": overflow == 0,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
