@@ -67,27 +67,36 @@ def load_traffic(workload: dict):
     return None
 
 
-def cpu_baseline(args, kw, log_cap):
+def cpu_baseline(args, kw, log_cap, total_steps):
     """Oracle (scalar C restatement of the reference) on a bounded sample of
-    the same workload, on this host's cores (rank 0, N=1 only)."""
+    the same workload, on this host's cores (rank 0, N=1 only).  The sample
+    is a contiguous range of the same global groups, run for the same number
+    of steps as the GPU (so logs grow exactly as they do there); its size is
+    calibrated so that the timed part takes about --cpu-seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    G = args.cpu_groups
-    o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
-    o.step(args.warmup_cpu, nthreads=threads, counters=False)
+    # calibration: a short run of a small sample
+    probe = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=args.cpu_groups)))
     t0 = time.perf_counter()
-    n = 0
-    while True:
-        o.step(args.cpu_chunk, nthreads=threads, counters=True)
-        n += args.cpu_chunk
-        if time.perf_counter() - t0 >= args.cpu_seconds:
-            break
+    probe.step(args.cpu_chunk, nthreads=threads, counters=False)
+    rate = args.cpu_groups * args.cpu_chunk / max(1e-6, time.perf_counter() - t0)
+    probe.close()
+    G = int(min(kw["G"], max(threads * 64, rate * args.cpu_seconds / total_steps)))
+    o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
+    o.step(args.warmup, nthreads=threads, counters=False)
+    t0 = time.perf_counter()
+    done = 0
+    while done < total_steps - args.warmup:
+        k = min(args.cpu_chunk * 10, total_steps - args.warmup - done)
+        o.step(k, nthreads=threads, counters=True)
+        done += k
     dt = time.perf_counter() - t0
     o.close()
-    return {"value": G * n / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/raft_oracle.c, {G} groups x {n} steps of the same config "
-                      f"(after {args.warmup_cpu} warmup steps), {dt:.1f} s, pthreads over groups"}
+    return {"value": G * done / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/raft_oracle.c (scalar C restatement of RaftServer.kt/Commons.kt), global groups "
+                      f"0..{G - 1} of the same config for the same {total_steps} steps as the GPU "
+                      f"({args.warmup} untimed), {dt:.1f} s, pthreads over groups"}
 
 
 def main():
@@ -105,7 +114,7 @@ def main():
     ap.add_argument("--reduce-every", type=int, default=256, help="steps per counter all-reduce")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-groups", type=int, default=20_000)
+    ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-chunk", type=int, default=20)
@@ -264,7 +273,7 @@ def main():
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, kw, log_cap)
+        out["cpu_baseline"] = cpu_baseline(args, kw, log_cap, args.warmup + args.steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -43,9 +43,13 @@ RAFT_HD u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
     return u32x4{c0, c1, c2, c3};
 }
 
-RAFT_HD uint32_t word_of(const u32x4& v, int i) {
-    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+// Word i (0..3) as two bit-selects: a chain of i == k compares would be
+// lowered to a branchy switch on the GPU.
+RAFT_HD uint32_t sel4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int i) {
+    const uint32_t lo = (i & 1) ? b : a, hi = (i & 1) ? d : c;
+    return (i & 2) ? hi : lo;
 }
+RAFT_HD uint32_t word_of(const u32x4& v, int i) { return sel4(v.x, v.y, v.z, v.w, i); }
 
 // (lo..hi).random() (Commons.kt:33-34), scaled by multiply-shift (S-9)
 RAFT_HD int32_t scale_range(uint32_t w, int32_t lo, int32_t hi) {

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 // [k][NCW][nblocks].  One barrier (the LDS clear) per launch; waves of a
 // workgroup otherwise run free of each other.
 #ifndef RAFT_STEP_WAVES_PER_EU
-#define RAFT_STEP_WAVES_PER_EU 4
+#define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
 #endif
 template <int R>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
@@ -408,19 +408,19 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
         if (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt; bool gr;
-            vote_handler(x.ref(), q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
+            vote_handler(x.ref(), true, q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, gr ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
             int32_t rt = 0; bool su = false;
             const int32_t pv = q.prev_log_index;
             const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lr[pv].x : 0;
-            const bool okh = append_handler(x.ref(), r + 1, lr, p.cap, q.term, q.leader_id, pv,
+            const bool okh = append_handler(x.ref(), true, r + 1, lr, p.cap, q.term, q.leader_id, pv,
                                             q.prev_log_term, q.has_entry != 0, Entry{q.entry_term, q.entry_cmd},
                                             q.leader_commit, dprev, cnt, rt, su);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, su ? 1 : 0, okh ? 0 : 1};
         } else {
-            append_command(x.ref(), lr, p.cap, ((const uint32_t*)req)[o], cnt);
+            append_command(x.ref(), true, lr, p.cap, ((const uint32_t*)req)[o], cnt);
         }
         resolve_rep_draw(x, p, t, gid, r);
     }

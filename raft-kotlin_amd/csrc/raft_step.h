@@ -102,8 +102,10 @@ struct Counters {
     }
 #ifdef RAFT_EXP_NO_COUNTERS
     __device__ __forceinline__ void add(int) {}
+    __device__ __forceinline__ void add_if(bool, int) {}
 #else
     __device__ __forceinline__ void add(int c) { ev |= 1u << c; }
+    __device__ __forceinline__ void add_if(bool cond, int c) { ev |= (uint32_t)cond << c; }
 #endif
     template <uint32_t MASK>
     __device__ __forceinline__ void flush() {
@@ -131,14 +133,18 @@ struct Rep {
 };
 
 // ---- timer / consumer (Commons.kt:10-31, RaftServer.kt:50-69) -------------
-// reset(): re-arm with a fresh draw.  The draw is a pure function of
-// (step, group, replica), so it is resolved once at the end of the step no
-// matter how many resets the step performed (S-9).
-__device__ __forceinline__ void reset_timer(Rep n) { n.fl |= FL_ARMED | FL_DRAW; }
-// launch { channel.send(FOLLOWER) } (RaftServer.kt:241, :261, :266), S-5
-__device__ __forceinline__ void send_follower(Rep n) {
-    if (n.fl & FL_ELECTING) n.fl |= FL_PRST; else reset_timer(n);
+// `launch { channel.send(FOLLOWER) }` (RaftServer.kt:241, :261, :266), S-5: an
+// idle consumer re-arms the timer (reset() with a fresh draw, resolved once
+// at the end of the step because the draw is a pure function of (step, group,
+// replica), S-9); a consumer busy in leaderElection() queues the reset.
+__device__ __forceinline__ uint32_t follower_sent(uint32_t fl) {
+    return (fl & FL_ELECTING) ? FL_PRST : (FL_ARMED | FL_DRAW);
 }
+
+// The handlers below are written as predicated selects (applied iff `act`)
+// with at most one optional load and one optional store, not as nested ifs:
+// in SIMT every branch side costs the whole wave, and branch merges cost
+// register copies.  Semantics are exactly the reference's (cited per line).
 
 // ---- Log<T> (Commons.kt:47-74) over one replica's HBM slots ---------------
 // The 2-deep tail cache answers every steady-state read (prev checks, the
@@ -149,94 +155,87 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
     return j == last - 1 ? t1 : t2;
 }
 
-// Log.add(i, e): 1 true, 0 false, -1 capacity overflow (counted), -2 threw
-__device__ __forceinline__ int log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e) {
-    if (n.last == i) {                                 // :58-61 append at the PHYSICAL end (Q1)
-        if (n.phys >= cap) return -1;
-        lr[n.phys] = make_uint2((uint32_t)e.term, e.cmd);
-        if (n.phys == n.last) {                        // no ghost: the new last entry is e
-            n.t2 = n.t1; n.t1 = e.term; n.c1 = e.cmd;
-        } else {                                       // ghost: stale slot log[last] resurfaces
-            const uint2 gs = lr[n.last];
-            n.t2 = n.t1; n.t1 = (int32_t)gs.x; n.c1 = gs.y;
-        }
-        n.phys += 1;
-        n.last += 1;
-        return 1;
-    }
-    if (n.last < i) return 0;                          // :62
-    if (i < 0) return -2;
-    lr[i] = make_uint2((uint32_t)e.term, e.cmd);       // :63-66 overwrite, no shrink
-    // new last = i + 1; log[i-1] is unchanged
-    n.t2 = i == 0 ? 0 : (i == n.last - 1 ? n.t2 : (int32_t)lr[i - 1].x);
-    n.t1 = e.term;
-    n.c1 = e.cmd;
-    n.last = i + 1;
-    return 1;
+// Log.add(i, e) for 0 <= i <= lastIndex, the only indices its callers pass:
+// appendCommand adds at lastIndex, and append() adds at prevLogIndex + 1 only
+// after the consistency check passed (prevLogIndex == -1 or < lastIndex).
+//   i == lastIndex: :58-61, log.add(entry) appends at the PHYSICAL end (Q1);
+//   i <  lastIndex: :63-66, log[i] = entry, lastIndex = i + 1, no shrink.
+// The build refuses an append beyond log_cap (counted, never wrapped).
+__device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e, bool act, bool& wrote,
+                                        bool& overflow) {
+    const int32_t last = n.last, phys = n.phys;
+    const bool app = i == last;
+    const bool ghost = app && phys != last;            // the stale slot log[last] becomes the last entry
+    overflow = act && app && phys >= cap;
+    wrote = act && !overflow;
+    // the one slot the new tail cache needs from HBM
+    const bool ld = wrote && (ghost || (!app && i >= 1 && i != last - 1));
+    uint2 g = make_uint2(0u, 0u);
+    if (ld) g = lr[app ? last : i - 1];
+    if (wrote) lr[app ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
+    const int32_t t1 = app ? (ghost ? (int32_t)g.x : e.term) : e.term;
+    const uint32_t c1 = app ? (ghost ? g.y : e.cmd) : e.cmd;
+    const int32_t t2 = app ? n.t1 : (i == 0 ? 0 : (i == last - 1 ? n.t2 : (int32_t)g.x));
+    n.t1 = wrote ? t1 : n.t1;
+    n.c1 = wrote ? c1 : n.c1;
+    n.t2 = wrote ? t2 : n.t2;
+    n.phys = wrote && app ? phys + 1 : phys;
+    n.last = wrote ? i + 1 : last;
 }
 
-// ---- vote() (RaftServer.kt:228-251) ---------------------------------------
-__device__ __forceinline__ void vote_handler(Rep n, int32_t rt, int32_t rc, int32_t rli, int32_t rlt, Counters& cnt,
-                                             int32_t& resp_term, bool& granted) {
-    granted = false;
-    if (rt < n.term) {
-    } else if (n.term == rt) {
-        granted = n.voted == rc;
-    } else {
-        int32_t lt = 0;
-        if (n.last >= 1) { lt = n.t1; cnt.add(RAFT_C_VOTE_LOG_READS); }
-        if (n.last >= 1 && rlt < lt) {
-        } else if (n.last >= 1 && rlt == lt && rli < n.last) {
-        } else {
-            n.term = rt; n.voted = rc; n.role = RAFT_FOLLOWER;
-            send_follower(n);
-            granted = true;
-        }
-    }
-    if (granted) cnt.add(RAFT_C_VOTES_GRANTED);
-    resp_term = n.term;
+// ---- vote() (RaftServer.kt:228-251), applied iff act ----------------------
+__device__ __forceinline__ void vote_handler(Rep n, bool act, int32_t rt, int32_t rc, int32_t rli, int32_t rlt,
+                                             Counters& cnt, int32_t& resp_term, bool& granted) {
+    const bool higher = rt > n.term;                                            // :229-231
+    const bool hasl = n.last >= 1;
+    const bool logrej = hasl && (rlt < n.t1 || (rlt == n.t1 && rli < n.last));  // :232-236 (Q5)
+    const bool up = act && higher && !logrej;                                   // :237-242
+    granted = up || (act && rt == n.term && n.voted == rc);                     // :230
+    cnt.add_if(act && higher && hasl, RAFT_C_VOTE_LOG_READS);
+    cnt.add_if(granted, RAFT_C_VOTES_GRANTED);
+    n.fl |= up ? follower_sent(n.fl) : 0u;                                      // :241
+    n.term = up ? rt : n.term;
+    n.voted = up ? rc : n.voted;
+    n.role = up ? (int32_t)RAFT_FOLLOWER : n.role;
+    resp_term = n.term;                                                         // :246-249
 }
 
-// ---- append() (RaftServer.kt:253-287); returns false where it throws -------
-// dprev = term of this replica's log[prev], read by the caller ahead of time
-// (valid whenever 0 <= prev < lastIndex, the only case it is used).
-__device__ __forceinline__ bool append_handler(Rep n, int32_t id, uint2* lr, int cap, int32_t rt, int32_t rlead,
-                                               int32_t prev, int32_t prevTerm, bool has, Entry e,
+// ---- append() (RaftServer.kt:253-287), applied iff act --------------------
+// Returns false where the reference throws (Log.get with prevLogIndex < -1):
+// that call has no response.  dprev = term of this replica's log[prev], read
+// by the caller ahead of time (valid whenever 0 <= prev < lastIndex).
+__device__ __forceinline__ bool append_handler(Rep n, bool act, int32_t id, uint2* lr, int cap, int32_t rt,
+                                               int32_t rlead, int32_t prev, int32_t prevTerm, bool has, Entry e,
                                                int32_t lcommit, int32_t dprev, Counters& cnt, int32_t& resp_term,
                                                bool& success) {
-    if (rt > n.term) {                                  // :257-262
-        n.term = rt; n.voted = -1; n.role = RAFT_FOLLOWER;
-        send_follower(n);
-    }
-    if (rlead != id) {                                  // :264-268 (Q3)
-        n.role = RAFT_FOLLOWER;
-        send_follower(n);
-    }
-    if (lcommit > n.commit) {                           // :270-272 (Q4)
-        const int32_t c = min(lcommit, n.last);
-        if (c < n.commit) cnt.add(RAFT_C_COMMIT_REGRESSIONS);
-        n.commit = c;
-    }
-    if (prev == -1) success = true;                     // :274-276
-    else if (n.last > prev) {
-        if (prev < 0) { resp_term = n.term; success = false; return false; }
-        cnt.add(RAFT_C_PREV_READS_FOLLOWER);
-        success = dprev == prevTerm;
-    } else success = false;
-    if (success && has) {                               // :278 (Q2, Q10)
-        const int r = log_add(lr, cap, n, prev + 1, e);
-        if (r == 1) cnt.add(RAFT_C_ENTRY_WRITES);
-        else if (r == -1) cnt.add(RAFT_C_LOG_OVERFLOW);
-    }
-    resp_term = n.term;
-    return true;
+    const bool up = act && rt > n.term;                                         // :257-262
+    const bool fol = up || (act && rlead != id);                                // :264-268 (Q3)
+    n.fl |= fol ? follower_sent(n.fl) : 0u;
+    n.term = up ? rt : n.term;
+    n.voted = up ? -1 : n.voted;
+    n.role = fol ? (int32_t)RAFT_FOLLOWER : n.role;
+    const bool cu = act && lcommit > n.commit;                                  // :270-272 (Q4)
+    const int32_t cc = min(lcommit, n.last);
+    cnt.add_if(cu && cc < n.commit, RAFT_C_COMMIT_REGRESSIONS);
+    n.commit = cu ? cc : n.commit;
+    const bool check = prev != -1 && n.last > prev;                             // :274-276
+    const bool thrown = check && prev < 0;
+    cnt.add_if(act && check && !thrown, RAFT_C_PREV_READS_FOLLOWER);
+    success = act && (prev == -1 || (check && !thrown && dprev == prevTerm));
+    bool wrote, ovf;
+    log_add(lr, cap, n, prev + 1, e, success && has, wrote, ovf);               // :278 (Q2, Q10)
+    cnt.add_if(wrote, RAFT_C_ENTRY_WRITES);
+    cnt.add_if(ovf, RAFT_C_LOG_OVERFLOW);
+    resp_term = n.term;                                                         // :282-285
+    return !thrown;
 }
 
-// ---- appendCommand() (RaftServer.kt:100-107) ------------------------------
-__device__ __forceinline__ void append_command(Rep n, uint2* lr, int cap, uint32_t cmd, Counters& cnt) {
-    const int r = log_add(lr, cap, n, n.last, Entry{n.term, (uint32_t)cmd});
-    cnt.add(RAFT_C_COMMANDS);
-    if (r == -1) cnt.add(RAFT_C_LOG_OVERFLOW);
+// ---- appendCommand() (RaftServer.kt:100-107), applied iff act -------------
+__device__ __forceinline__ void append_command(Rep n, bool act, uint2* lr, int cap, uint32_t cmd, Counters& cnt) {
+    bool wrote, ovf;
+    log_add(lr, cap, n, n.last, Entry{n.term, cmd}, act, wrote, ovf);
+    cnt.add_if(act, RAFT_C_COMMANDS);
+    cnt.add_if(ovf, RAFT_C_LOG_OVERFLOW);
 }
 
 // ---------------------------------------------------------------------------
@@ -308,11 +307,10 @@ struct Ctx {
 
 template <int R>
 __device__ __forceinline__ bool lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
-    if (s == d) return false;                                      // S-7
-    if (c.iso >= 0 && (s == c.iso || d == c.iso)) return true;
-    if (((c.part >> s) ^ (c.part >> d)) & 1u) return true;
-    if (p.drop_thr16 == 0) return false;
-    return ((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16;             // uniform j = 2*dd + b: word dd, half b
+    const bool iso = c.iso >= 0 && (s == c.iso || d == c.iso);                 // churn isolation
+    const bool part = ((c.part >> s) ^ (c.part >> d)) & 1u;                     // partition sides
+    const bool drop = ((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16;              // uniform j = 2*dd + b: word dd, half b
+    return s != d && (iso || part || drop);                                     // S-7: self never lost
 }
 
 // 16-bit drop uniforms of sender s for this lane as destination d (S-9):
@@ -337,7 +335,7 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int 
     const int sl = c.src(job_lane);
     const uint32_t a = bcastu(c.job.x, sl), b = bcastu(c.job.y, sl);
     const uint32_t x = bcastu(c.job.z, sl), y = bcastu(c.job.w, sl);
-    return k == 0 ? a : k == 1 ? b : k == 2 ? x : y;
+    return sel4(a, b, x, y, k);
 }
 
 template <int R, bool HAVE_JOB>
@@ -400,42 +398,15 @@ struct Stepper {
         n.mc = p.spill[p.GR * R + c.idx * R + s];
     }
 
-    // while (state == CANDIDATE) iteration head (RaftServer.kt:191-199): the
-    // RequestVote snapshot is built inside retry{} (:200-207)
-    __device__ __forceinline__ static void build_vote_request(Node& n, Counters& cnt, int32_t& qt, int32_t& qli,
-                                                              int32_t& qlt) {
-        qt = n.term;
-        qli = n.last;
-        qlt = 0;
-        if (n.last != 0) { qlt = n.t1; cnt.add(RAFT_C_VOTE_LOG_READS); }
-    }
-    __device__ __forceinline__ static void start_round(Node& n, int r, Counters& cnt, uint32_t& send, int32_t& qt,
-                                                       int32_t& qli, int32_t& qlt) {
-        n.term += 1;                                                      // :192
-        n.voted = r + 1;                                                  // :193
-        n.fl = (n.fl & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
-               (ALL << PEND_SH);
-        n.phase = 0;
-        n.retry = 0;
-        send = ALL;
-        build_vote_request(n, cnt, qt, qli, qlt);
-        cnt.add(RAFT_C_ROUNDS);
-    }
-
-    // leaderElection() returns; queued sends then the final state (S-5).
-    // Returns true when the final state is LEADER: the caller starts the
-    // heartbeat session (RaftServer.kt:66) in group order.
-    __device__ __forceinline__ static bool end_election(Node& n) {
-        uint32_t f = n.fl;
+    // The flags after leaderElection() returns (S-5): the queued FOLLOWER
+    // send first, then the final state -- LEADER starts the heartbeat session
+    // (RaftServer.kt:66), FOLLOWER re-arms the timer (:64).
+    __device__ __forceinline__ static uint32_t end_flags(uint32_t f, int32_t role) {
         const bool prst = f & FL_PRST;
         f &= ~(FL_ELECTING | FL_PRST | FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH));
-        if (prst) f |= FL_ARMED | FL_DRAW;
-        n.fl = f;
-        n.phase = 0;
-        n.retry = 0;
-        if (n.role == RAFT_LEADER) { n.fl |= FL_HB; return true; }       // :66
-        if (n.role == RAFT_FOLLOWER) n.fl |= FL_ARMED | FL_DRAW;         // :64
-        return false;
+        f |= prst ? (FL_ARMED | FL_DRAW) : 0u;
+        f |= role == RAFT_LEADER ? FL_HB : (role == RAFT_FOLLOWER ? (FL_ARMED | FL_DRAW) : 0u);
+        return f;
     }
 
     // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113) for every
@@ -484,16 +455,15 @@ struct Stepper {
 
         // build this destination's request (RaftServer.kt:122-132)
         const int32_t i = n.nx, prev = i - 2;
-        bool ok = true, has = false;
-        if (prev >= 0) {                                                  // :128 (Q11)
-            if (prev > Llast - 1) ok = false;
-            else cnt.add(RAFT_C_PREV_READS_LEADER);
-        }
-        if (ok && Llast >= i) {                                           // :130-131
-            if (i - 1 < 0) ok = false;
-            else { has = true; cnt.add(RAFT_C_ENTRY_READS_LEADER); }
-        }
-        if (!ok) cnt.add(RAFT_C_APPEND_SKIPPED);
+        const bool pv = prev >= 0;
+        const bool pv_bad = pv && prev > Llast - 1;                     // :128 Log.get throws (Q11)
+        const bool has_c = !pv_bad && Llast >= i;                         // :130
+        const bool ent_bad = has_c && i - 1 < 0;                          // :131 throws
+        const bool has = has_c && !ent_bad;
+        const bool ok = !pv_bad && !ent_bad;
+        cnt.add_if(pv && !pv_bad, RAFT_C_PREV_READS_LEADER);
+        cnt.add_if(has, RAFT_C_ENTRY_READS_LEADER);
+        cnt.add_if(!ok, RAFT_C_APPEND_SKIPPED);
         // every log slot of the tick, resolved up front: the leader's log[prev]
         // and log[i-1], and this replica's own log[prev] (append() :274-276);
         // a handler only writes its own replica's log, so no handler of the
@@ -511,20 +481,16 @@ struct Stepper {
         if (ld3) dpt = (int32_t)c.lr[prev].x;
 
         const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, s, L::J_TICK, c.s_tick);
-        bool lreq = false, lresp = false, delivered = false, succ = false;
-        int32_t rterm = 0;
-        if (ok) {
-            cnt.add(RAFT_C_APPEND_SENT);
-            lreq = lost(p, c, s, c.r, dw, 0);                             // :170-172
-            if (!lreq) {
-                if (append_handler(n.rep(), c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
-                                   Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ)) {
-                    lresp = lost(p, c, s, c.r, dw, 1);
-                    delivered = !lresp;
-                }
-            }
-        }
-        if (lreq | lresp) cnt.add(RAFT_C_MSG_DROPPED);
+        cnt.add_if(ok, RAFT_C_APPEND_SENT);
+        const bool lreq = ok && lost(p, c, s, c.r, dw, 0);                // :170-172
+        const bool act = ok && !lreq;
+        int32_t rterm;
+        bool succ;
+        const bool answered = append_handler(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
+                                             Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ);
+        const bool lresp = act && answered && lost(p, c, s, c.r, dw, 1);
+        const bool delivered = act && answered && !lresp;
+        cnt.add_if(lreq || lresp, RAFT_C_MSG_DROPPED);
 
         // responses in destination order (S-4).  :146-154 (Q7): a response
         // with a term above the running term adopts it and skips the rest of
@@ -542,15 +508,13 @@ struct Stepper {
             }
         }
         const int32_t mc_old = n.mc;
-        bool chk = false;
-        if (delivered && !sdb) {
-            if (succ) {                                                   // :156-165 (Q9)
-                if (has) { n.nx += 1; n.mc += 1; cnt.add(RAFT_C_ENTRIES_ACKED); chk = true; }
-                else n.mc = prev + 1;                                     // :164
-            } else {
-                n.nx -= 1;                                                // :167
-            }
-        }
+        const bool nd = delivered && !sdb;
+        const bool chk = nd && succ && has;                               // :156-162 (Q9)
+        const bool hbk = nd && succ && !has;                              // :163-164
+        const bool nak = nd && !succ;                                     // :166-167
+        n.nx += chk ? 1 : (nak ? -1 : 0);
+        n.mc = chk ? mc_old + 1 : (hbk ? prev + 1 : mc_old);
+        cnt.add_if(chk, RAFT_C_ENTRIES_ACKED);
         // commit rule, after each acknowledged entry in destination order:
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;
@@ -562,20 +526,17 @@ struct Stepper {
                 if (!(ckb & L::lanes_of(q))) continue;                    // wave-uniform
                 const int32_t cur = c.r <= q ? n.mc : mc_old;             // rows after / before response q
                 const uint32_t gt = c.gbits(__ballot(cur > C));           // :161
-                if (((ck >> q) & 1u) && __popc(gt) >= MAJ) {              // :162
-                    C += 1;
-                    if (c.r == q) cnt.add(RAFT_C_COMMITS);
-                }
+                const bool inc = ((ck >> q) & 1u) && __popc(gt) >= MAJ;  // :162
+                C += inc ? 1 : 0;
+                cnt.add_if(inc && c.r == q, RAFT_C_COMMITS);
             }
         }
-        if (c.r == s) {
-            n.term = T;
-            n.commit = C;
-            if (stepdown) {                                               // :148 + offer(FOLLOWER) :152 (S-6)
-                n.role = RAFT_FOLLOWER;
-                if (!(n.fl & FL_ELECTING)) n.fl |= FL_ARMED | FL_DRAW;
-            }
-        }
+        const bool me = c.r == s;
+        const bool sd = me && stepdown;                                   // :148 + offer(FOLLOWER) :152 (S-6)
+        n.term = me ? T : n.term;
+        n.commit = me ? C : n.commit;
+        n.role = sd ? (int32_t)RAFT_FOLLOWER : n.role;
+        n.fl |= (sd && !(n.fl & FL_ELECTING)) ? (FL_ARMED | FL_DRAW) : 0u;
     }
 
     // One RequestVote round: every group with a pending sender delivers the
@@ -592,29 +553,26 @@ struct Stepper {
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
         const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, L::J_VOTE, c.s_vote);
-        bool lreq = false, lresp = false, delivered = false, granted = false;
-        int32_t rterm = 0;
-        if ((ms >> r) & 1u) {
-            lreq = lost(p, c, s, r, dw, 0);                         // retry{} swallows, Commons.kt:41
-            if (!lreq) {
-                vote_handler(n.rep(), rt, s + 1, rli, rlt, cnt, rterm, granted);
-                lresp = lost(p, c, s, r, dw, 1);
-                delivered = !lresp;
-            }
-        }
-        if (lreq | lresp) cnt.add(RAFT_C_MSG_DROPPED);
+        const bool mine = (ms >> r) & 1u;
+        const bool lreq = mine && lost(p, c, s, r, dw, 0);          // retry{} swallows, Commons.kt:41
+        const bool act = mine && !lreq;
+        int32_t rterm;
+        bool granted;
+        vote_handler(n.rep(), act, rt, s + 1, rli, rlt, cnt, rterm, granted);
+        const bool lresp = act && lost(p, c, s, r, dw, 1);
+        const bool delivered = act && !lresp;
+        cnt.add_if(lreq || lresp, RAFT_C_MSG_DROPPED);
         // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
         const uint32_t dl = c.gbits(__ballot(delivered));
         const uint32_t gr = c.gbits(__ballot(delivered && granted));
         const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
-        if (r == s) {
-            uint32_t f = n.fl & ~(dl << PEND_SH);
-            f += (uint32_t)__popc(dl) << LATCH_SH;                  // :209 countDown()
-            f += (uint32_t)__popc(gr) << VOTES_SH;                  // :211
-            n.fl = f;
-            if (hi) n.role = RAFT_FOLLOWER;                         // :210 (Q6)
-            if ((f >> PEND_SH) & 0xFFu) n.retry = p.retry;
-        }
+        const bool me = r == s;
+        uint32_t f = n.fl & ~(dl << PEND_SH);
+        f += (uint32_t)__popc(dl) << LATCH_SH;                      // :209 countDown()
+        f += (uint32_t)__popc(gr) << VOTES_SH;                      // :211
+        n.fl = me ? f : n.fl;
+        n.role = (me && hi) ? (int32_t)RAFT_FOLLOWER : n.role;     // :210 (Q6)
+        n.retry = (me && ((f >> PEND_SH) & 0xFFu)) ? p.retry : n.retry;
     }
 
     // One lockstep step of every group of the wave.
@@ -627,41 +585,46 @@ struct Stepper {
         const uint32_t lead0 = c.gbits(__ballot(n.role == RAFT_LEADER));
 
         // ---------------- T: timers and election clocks ----------------
-        uint32_t send = 0;
-        int32_t qt = 0, qli = 0, qlt = 0;
-        bool sstart = false;
+        uint32_t send;
+        int32_t qt, qli, qlt;
+        bool sstart;
         {
-            bool started = false;
-            if (n.fl & FL_ARMED) {
-                n.elec -= p.P;
-                if (n.elec <= 0) {                                          // Commons.kt:25-27
-                    n.fl &= ~FL_ARMED;
-                    n.elec = 0;
-                    cnt.add(RAFT_C_TIMEOUTS);
-                    n.role = RAFT_CANDIDATE;                                // RaftServer.kt:182
-                    if (!(n.fl & FL_ELECTING)) {                            // :184 -> :65
-                        n.fl |= FL_ELECTING;
-                        start_round(n, r, cnt, send, qt, qli, qlt);
-                        started = true;
-                    }
-                }
-            }
-            if ((n.fl & FL_ELECTING) && !started) {
-                if (!(n.fl & FL_BACKOFF)) {
-                    n.phase += p.P;                                         // latch clock :214
-                    const uint32_t pend = (n.fl >> PEND_SH) & 0xFFu;
-                    if (pend && n.phase < p.round_to) {
-                        n.retry -= p.P;                                     // Commons.kt:43
-                        if (n.retry <= 0) { build_vote_request(n, cnt, qt, qli, qlt); send = pend; }
-                    }
-                } else {
-                    n.phase -= p.P;                                         // delay(backoff) :221
-                    if (n.phase <= 0) {
-                        if (n.role == RAFT_CANDIDATE) start_round(n, r, cnt, send, qt, qli, qlt);   // :191
-                        else sstart = end_election(n);
-                    }
-                }
-            }
+            uint32_t f = n.fl;
+            const bool armed = f & FL_ARMED;
+            const int32_t el = n.elec - p.P;
+            const bool fire = armed && el <= 0;                             // Commons.kt:25-27
+            n.elec = armed ? (fire ? 0 : el) : n.elec;
+            f &= fire ? ~FL_ARMED : ~0u;
+            n.role = fire ? (int32_t)RAFT_CANDIDATE : n.role;               // RaftServer.kt:182
+            cnt.add_if(fire, RAFT_C_TIMEOUTS);
+            const bool electing = f & FL_ELECTING;
+            const bool start_fire = fire && !electing;                      // offer(CANDIDATE) :184 -> :65
+            const bool in_round = electing && !(f & FL_BACKOFF);
+            const bool in_bo = electing && (f & FL_BACKOFF);
+            const int32_t ph = n.phase + (in_round ? p.P : (in_bo ? -p.P : 0));   // latch clock :214 / delay :221
+            const uint32_t pend = (f >> PEND_SH) & 0xFFu;
+            const bool rtick = in_round && pend && ph < p.round_to;
+            const int32_t rty = n.retry - (rtick ? p.P : 0);               // retry delay, Commons.kt:43
+            const bool resend = rtick && rty <= 0;
+            const bool bo_end = in_bo && ph <= 0;
+            const bool restart = bo_end && n.role == RAFT_CANDIDATE;        // while (state == CANDIDATE) :191
+            const bool endel = bo_end && !restart;
+            const bool sr = start_fire || restart;                          // round head :191-199
+            n.term += sr ? 1 : 0;                                           // :192
+            n.voted = sr ? r + 1 : n.voted;                                 // :193
+            const uint32_t fr = (f & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
+                                (ALL << PEND_SH) | (start_fire ? FL_ELECTING : 0u);
+            n.fl = sr ? fr : (endel ? end_flags(f, n.role) : f);
+            n.phase = (sr || endel) ? 0 : ph;
+            n.retry = (sr || endel) ? 0 : rty;
+            sstart = endel && n.role == RAFT_LEADER;
+            send = sr ? ALL : (resend ? pend : 0u);
+            // the RequestVote snapshot, built inside retry{} (:200-207)
+            qt = n.term;
+            qli = n.last;
+            qlt = n.last != 0 ? n.t1 : 0;
+            cnt.add_if((sr || resend) && n.last != 0, RAFT_C_VOTE_LOG_READS);
+            cnt.add_if(sr, RAFT_C_ROUNDS);
         }
         start_sessions(p, c, n, sstart, cnt);
         cnt.flush<M_T>();
@@ -733,23 +696,22 @@ struct Stepper {
         }
 
         // ---------------- D: latch closes -> decision (RaftServer.kt:214-222) ----------------
-        bool dstart = false, need_bo = false;
+        bool dstart, need_bo;
         {
             const uint32_t f = n.fl;
             const int latch = (f >> LATCH_SH) & 0xF, votes = (f >> VOTES_SH) & 0xF;
-            if ((f & FL_ELECTING) && !(f & FL_BACKOFF) && (latch >= MAJ || n.phase >= p.round_to)) {
-                n.fl = f & ~(0xFFu << PEND_SH);                             // cancelChildren() :215
-                if (n.role == RAFT_CANDIDATE && votes >= MAJ) {             // :218-219
-                    n.role = RAFT_LEADER;
-                    dstart = end_election(n);
-                } else if (n.role == RAFT_CANDIDATE) {                      // :220-221
-                    n.fl = (n.fl & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
-                    n.retry = 0;
-                    need_bo = true;
-                } else {
-                    dstart = end_election(n);
-                }
-            }
+            const bool dec = (f & FL_ELECTING) && !(f & FL_BACKOFF) && (latch >= MAJ || n.phase >= p.round_to);
+            const bool cand = n.role == RAFT_CANDIDATE;
+            const bool win = dec && cand && votes >= MAJ;                   // :218-219
+            need_bo = dec && cand && votes < MAJ;                           // :220-221
+            const bool endel = dec && !need_bo;
+            const uint32_t fc = f & ~(0xFFu << PEND_SH);                    // cancelChildren() :215
+            n.role = win ? (int32_t)RAFT_LEADER : n.role;
+            const uint32_t fb = (fc & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
+            n.fl = endel ? end_flags(fc, n.role) : (need_bo ? fb : f);
+            n.phase = endel ? 0 : n.phase;
+            n.retry = dec ? 0 : n.retry;
+            dstart = endel && n.role == RAFT_LEADER;
         }
         if (__ballot(need_bo)) {
             const uint32_t w = timer_word(p, c);
@@ -781,7 +743,7 @@ struct Stepper {
             if ((p.cmd_limit == 0 || n.cmdc < p.cmd_limit) && hw1 < p.cmd_thr32 && lead) {
                 const bool tgt = p.cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
                                                                       : ((lead >> r) & 1u) != 0;
-                if (tgt) append_command(n.rep(), c.lr, p.cap, hw2, cnt);
+                append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
                 n.cmdc++;
             }
             cnt.flush<M_C>();

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-R step_kernel ISA statistics (VGPRs, SGPR spills via v_readlane/v_writelane, code size).
 set -e
-D=${1:-/tmp/isa}; mkdir -p $D; cd $D; rm -f raft_engine-*
+D=${1:-$PWD/gpurun_out/isa}; mkdir -p $D; cd $D; rm -f raft_engine-*
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared ${EXTRA:-} -I /root/repo/include --save-temps \
     -o $D/x.so /root/repo/raft-kotlin_amd/csrc/raft_engine.hip 2>&1 | grep -v warning | head -5 || true
 python3 - "$D" "${KERNEL:-step_kernel}" <<'PY'
