@@ -186,9 +186,11 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         // of the step loop, and each one pins an SGPR pair for the whole
         // kernel (spilled to VGPR lanes and reloaded at every use).
         asm volatile("" : "+v"(c.r), "+v"(c.base));
-        if (p.part_period > 0) {                                          // S-11 partitions
-            const uint32_t ph = t % (uint32_t)p.part_period;
-            if ((int64_t)ph < p.part_len) {
+        const KernArgs kp = kernargs();
+        const int32_t pperiod = kp->part_period;
+        if (pperiod > 0) {                                                // S-11 partitions
+            const uint32_t ph = t % (uint32_t)pperiod;
+            if ((int64_t)ph < kp->part_len) {
                 if (k == 0 || ph == 0) c.part = draw(p, t - ph, c.gid, RAFT_RNG_PARTITION, 0).x & L::ALL;
             } else {
                 c.part = 0;
@@ -208,7 +210,12 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         if (arrived == WAVES_PER_BLOCK - 1 && lane < NCW)                  // last wave of the block
             partials[((int64_t)k * NCW + lane) * gridDim.x + blockIdx.x] = slot[lane];
     }
-    if (live) store_node(n, p, g, c.idx, r == 0);
+    if (live) {
+        const KernArgs kp = kernargs();            // state pointers re-read, not kept live across the loop
+        DevParams q;
+        q.st = kp->st; q.ses = kp->ses; q.gx = kp->gx; q.GR = kp->GR; q.G = kp->G;
+        store_node(n, q, g, c.idx, r == 0);
+    }
 }
 
 // (re)derive the log-tail cache from lastIndex and the log (after host writes)

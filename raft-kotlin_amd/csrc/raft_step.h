@@ -86,6 +86,19 @@ struct DevParams {
 
 struct Entry { int32_t term; uint32_t cmd; };
 
+// The step kernel's DevParams as seen through the kernarg segment (constant
+// address space, so every field read is one scalar load).  Rarely used
+// fields are re-read through an opaque pointer where they are needed: kept
+// live across the step loop they would pin SGPRs, which the kernel would
+// spill into VGPR lanes and reload with v_readlane at every use.
+// Valid only inside step_kernel, whose first kernel argument is the DevParams.
+typedef const __attribute__((address_space(4))) DevParams* KernArgs;
+__device__ __forceinline__ KernArgs kernargs() {
+    KernArgs kp = (KernArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return kp;
+}
+
 // Step counters.  A handler marks an event in its lane's bit mask `ev` (bit
 // c = counter c; every counter fires at most once per lane between two
 // flushes).  flush<MASK>() -- called at wave-uniform points -- adds
@@ -389,13 +402,19 @@ struct Stepper {
     static constexpr uint32_t ALL = L::ALL;
 
     // ---- session rows (S-8): the primary lives in n.nx / n.mc, the others in spill
-    __device__ __forceinline__ static void spill_store(const DevParams& p, const Ctx<R>& c, const Node& n, int s) {
-        p.spill[c.idx * R + s] = n.nx;
-        p.spill[p.GR * R + c.idx * R + s] = n.mc;
+    // (rare: a session other than the primary starts or ticks; the spill
+    // base is re-read from the kernarg segment, see kernargs())
+    __device__ __forceinline__ static void spill_store(const DevParams&, const Ctx<R>& c, const Node& n, int s) {
+        const KernArgs kp = kernargs();
+        int32_t* sp = kp->spill;
+        sp[c.idx * R + s] = n.nx;
+        sp[kp->GR * R + c.idx * R + s] = n.mc;
     }
-    __device__ __forceinline__ static void spill_load(const DevParams& p, const Ctx<R>& c, Node& n, int s) {
-        n.nx = p.spill[c.idx * R + s];
-        n.mc = p.spill[p.GR * R + c.idx * R + s];
+    __device__ __forceinline__ static void spill_load(const DevParams&, const Ctx<R>& c, Node& n, int s) {
+        const KernArgs kp = kernargs();
+        const int32_t* sp = kp->spill;
+        n.nx = sp[c.idx * R + s];
+        n.mc = sp[kp->GR * R + c.idx * R + s];
     }
 
     // The flags after leaderElection() returns (S-5): the queued FOLLOWER
@@ -673,9 +692,12 @@ struct Stepper {
         {
             int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
             if (rem > 0) { rem--; if (rem == 0) rep = 0; }
-            if (p.churn_thr32 && p.churn_steps > 0 && rem == 0 && hw0 < p.churn_thr32 && lead0) {
+            const KernArgs kp = kernargs();
+            const uint64_t thr = kp->churn_thr32;
+            const int32_t csteps = kp->churn_steps;
+            if (thr && csteps > 0 && rem == 0 && hw0 < thr && lead0) {
                 rep = __builtin_ctz(lead0);                                 // lowest-id LEADER
-                rem = p.churn_steps;
+                rem = csteps;
             }
             n.iso = rem > 0 ? (rem << 8) | rep : 0;
             c.iso = rem > 0 ? rep : -1;
@@ -715,7 +737,8 @@ struct Stepper {
         }
         if (__ballot(need_bo)) {
             const uint32_t w = timer_word(p, c);
-            if (need_bo) n.phase = scale_range(w, p.bmin, p.bmax);
+            const KernArgs kp = kernargs();
+            if (need_bo) n.phase = scale_range(w, kp->bmin, kp->bmax);
         }
         start_sessions(p, c, n, dstart, cnt);
         cnt.flush<M_D>();
@@ -738,10 +761,13 @@ struct Stepper {
         }
 
         // ---------------- C: client commands (S-11) ----------------
-        if (p.cmd_thr32) {
+        const KernArgs kp = kernargs();
+        const uint64_t cthr = kp->cmd_thr32;
+        if (cthr) {
+            const int32_t climit = kp->cmd_limit;
             const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
-            if ((p.cmd_limit == 0 || n.cmdc < p.cmd_limit) && hw1 < p.cmd_thr32 && lead) {
-                const bool tgt = p.cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
+            if ((climit == 0 || n.cmdc < climit) && hw1 < cthr && lead) {
+                const bool tgt = kp->cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
                                                                       : ((lead >> r) & 1u) != 0;
                 append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
                 n.cmdc++;

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_${TAG:-x}; mkdir -p "$OUT"
-B=${BENCH:-"bench.py --steps 128 --warmup 64 --no-cpu-baseline --steps-per-launch 64"}
+B=${BENCH:-"bench.py --steps 128 --warmup 64 --stream-steps 0 --no-cpu-baseline --steps-per-launch 64"}
 timeout -k 10 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1
 i=0
 IFS='|' read -ra PASSES <<< "${PMCS}"
