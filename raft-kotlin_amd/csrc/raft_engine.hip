@@ -35,6 +35,9 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 constexpr int BLOCK = 256;
+#ifdef RAFT_PROFILE_PHASES
+__device__ unsigned long long g_phase_cycles[PH_N];   // diagnostic builds only
+#endif
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 
 __device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
@@ -141,11 +144,10 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 }
 
 // K lockstep steps of every group.  A wave holds GPW whole groups, one lane
-// per replica.  Counters: each wave reduces its lanes' packed 16-bit pairs
-// (DPP), adds them into the workgroup's LDS slot of the step, and the last
-// wave of the workgroup to finish the step writes the workgroup's partials
-// [k][NCW][nblocks].  One barrier (the LDS clear) per launch; waves of a
-// workgroup otherwise run free of each other.
+// per replica.  Counters: a wave's totals of a step (SGPRs) go to its own LDS
+// row [k][wave][NCW] with one plain store -- no atomic, no wait in the step
+// loop -- and after the loop (the launch's only barrier) the workgroup sums
+// its waves' rows into the partials [k][NCW][nblocks].
 #ifndef RAFT_STEP_WAVES_PER_EU
 #define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
 #endif
@@ -154,11 +156,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
     using L = Lanes<R>;
-    extern __shared__ uint32_t lds_cnt[];                                 // [nsteps][NCW + 1]
-    for (int q = threadIdx.x; q < nsteps * (NCW + 1); q += BLOCK) lds_cnt[q] = 0;
-    __syncthreads();
+    extern __shared__ uint32_t lds_cnt[];                                 // [nsteps][WAVES_PER_BLOCK][NCW]
     const int lane = threadIdx.x & 63;
-    const int wid = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int wib = threadIdx.x >> 6;
+    const int wid = blockIdx.x * WAVES_PER_BLOCK + wib;
     const int j = lane / R;
     const int r = lane - j * R;
     const int64_t g = (int64_t)wid * L::GPW + j;
@@ -176,6 +177,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.job = u32x4{0u, 0u, 0u, 0u};
 
     Node n;
+    c.clk.start();
     if (live) load_node(n, p, g, c.idx);
     else inert_node(n);
     for (int k = 0; k < nsteps; ++k) {
@@ -199,17 +201,25 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         Counters cnt;
         cnt.clear();
         Stepper<R>::step(p, c, n, cnt);
-        uint32_t* slot = lds_cnt + k * (NCW + 1);
+        c.clk.mark(PH_TDRAW);
+        uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
-        for (int cw = 0; cw < NCW; ++cw) {                                  // wave totals (SGPRs)
-            if (lane == 0 && cnt.s[cw]) atomicAdd(&slot[cw], cnt.s[cw]);    // < 2^16 per half per block
-        }
-        uint32_t arrived = 0;
-        if (lane == 0) arrived = atomicAdd(&slot[NCW], 1u);
-        arrived = __shfl(arrived, 0, 64);
-        if (arrived == WAVES_PER_BLOCK - 1 && lane < NCW)                  // last wave of the block
-            partials[((int64_t)k * NCW + lane) * gridDim.x + blockIdx.x] = slot[lane];
+        for (int cw = 0; cw < NCW; ++cw) v = lane == cw ? cnt.s[cw] : v;
+        if (lane < NCW) lds_cnt[(k * WAVES_PER_BLOCK + wib) * NCW + lane] = v;
+        c.clk.mark(PH_CNT);
     }
+    __syncthreads();
+    for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK) {              // workgroup partials
+        const int k = q / NCW, cw = q - k * NCW;
+        uint32_t s = 0;                                                     // < 2^16 per half per block
+#pragma unroll
+        for (int w = 0; w < WAVES_PER_BLOCK; ++w) s += lds_cnt[(k * WAVES_PER_BLOCK + w) * NCW + cw];
+        partials[((int64_t)k * NCW + cw) * gridDim.x + blockIdx.x] = s;
+    }
+#ifdef RAFT_PROFILE_PHASES
+    if (lane == 0)
+        for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
+#endif
     if (live) {
         const KernArgs kp = kernargs();            // state pointers re-read, not kept live across the loop
         DevParams q;
@@ -482,7 +492,8 @@ template <int R> struct InitL {
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
-        step_kernel<R><<<e->nblocks, BLOCK, (size_t)k * (NCW + 1) * 4, e->stream>>>(e->dp, t0, k, e->partials);
+        step_kernel<R><<<e->nblocks, BLOCK, (size_t)k * WAVES_PER_BLOCK * NCW * 4, e->stream>>>(e->dp, t0, k,
+                                                                                             e->partials);
     }
 };
 template <int R> struct PackL {
@@ -615,6 +626,21 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
 
 int raft_engine_destroy(raft_engine* e) {
     if (!e) return RAFT_OK;
+#ifdef RAFT_PROFILE_PHASES
+    {
+        unsigned long long v[PH_N] = {0};
+        (void)hipSetDevice(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_phase_cycles), sizeof(v)) == hipSuccess) {
+            const char* names[PH_N] = {"T", "JOBS", "H", "V", "D", "A", "C", "K", "TDRAW", "CNT"};
+            unsigned long long tot = 0;
+            for (int q = 0; q < PH_N; ++q) tot += v[q];
+            fprintf(stderr, "[phase-cycles]");
+            for (int q = 0; q < PH_N; ++q) fprintf(stderr, " %s=%.1f%%", names[q], tot ? 100.0 * v[q] / tot : 0.0);
+            fprintf(stderr, " total=%llu\n", tot);
+        }
+    }
+#endif
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
     for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);

@@ -137,6 +137,28 @@ __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t 
     return philox4x32_10(c0, gid, purpose, sub, p.key0, p.key1);
 }
 
+// Phase timing (diagnostic builds only, -DRAFT_PROFILE_PHASES): s_memtime
+// deltas per step phase, summed per wave in SGPRs and added to a global
+// array at the end of the launch.  Never compiled into the product build.
+enum { PH_T = 0, PH_JOBS, PH_H, PH_V, PH_D, PH_A, PH_C, PH_K, PH_TDRAW, PH_CNT, PH_N };
+struct PhaseClock {
+#ifdef RAFT_PROFILE_PHASES
+    uint64_t last, acc[PH_N];
+    __device__ __forceinline__ void start() {
+        last = __builtin_amdgcn_s_memtime();
+        for (int k = 0; k < PH_N; ++k) acc[k] = 0;
+    }
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        acc[k] += now - last;
+        last = now;
+    }
+#else
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+#endif
+};
+
 // One replica's scalar state, by reference.
 struct Rep {
     int32_t &term, &voted, &role, &commit, &last, &phys, &elec, &phase, &retry;
@@ -310,6 +332,7 @@ struct Ctx {
     uint32_t part;            // replicas on side B of this step's partition
     uint2* lr;                // this replica's log
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS)
+    PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
 
     __device__ __forceinline__ uint32_t gbits(uint64_t b) const {
@@ -602,6 +625,11 @@ struct Stepper {
         // T draws no randomness, so it runs before the step's Philox pass and
         // that pass already knows the first RequestVote sender.
         const uint32_t lead0 = c.gbits(__ballot(n.role == RAFT_LEADER));
+        // harness parameters, read at step start (kernargs()) so the scalar
+        // loads are in flight while T runs
+        const KernArgs kp = kernargs();
+        const uint64_t churn_thr = kp->churn_thr32, cmd_thr = kp->cmd_thr32;
+        const int32_t churn_steps = kp->churn_steps, cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
 
         // ---------------- T: timers and election clocks ----------------
         uint32_t send;
@@ -647,6 +675,7 @@ struct Stepper {
         }
         start_sessions(p, c, n, sstart, cnt);
         cnt.flush<M_T>();
+        c.clk.mark(PH_T);
 
         // ---------------- the step's Philox pass (S-9) ----------------
         // lane J_HARNESS of a group: harness words; lanes J_TIMER..: timer
@@ -688,21 +717,20 @@ struct Stepper {
             if (x.x == 0x12345678u && x.y == 0x9ABCDEF0u && x.z == 1u) cnt.add(RAFT_C_LEADERS);
         }
 #endif
+        c.clk.mark(PH_JOBS);
         // ---------------- H: harness ----------------
         {
             int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
             if (rem > 0) { rem--; if (rem == 0) rep = 0; }
-            const KernArgs kp = kernargs();
-            const uint64_t thr = kp->churn_thr32;
-            const int32_t csteps = kp->churn_steps;
-            if (thr && csteps > 0 && rem == 0 && hw0 < thr && lead0) {
+            if (churn_thr && churn_steps > 0 && rem == 0 && hw0 < churn_thr && lead0) {
                 rep = __builtin_ctz(lead0);                                 // lowest-id LEADER
-                rem = csteps;
+                rem = churn_steps;
             }
             n.iso = rem > 0 ? (rem << 8) | rep : 0;
             c.iso = rem > 0 ? rep : -1;
         }
 
+        c.clk.mark(PH_H);
         // ---------------- V: RequestVote fan-out (S-3) ----------------
         // Each group walks its own senders in ascending order (group-uniform,
         // runtime s), so the wave runs as many rounds as its busiest group has
@@ -717,6 +745,7 @@ struct Stepper {
             }
         }
 
+        c.clk.mark(PH_V);
         // ---------------- D: latch closes -> decision (RaftServer.kt:214-222) ----------------
         bool dstart, need_bo;
         {
@@ -742,6 +771,7 @@ struct Stepper {
         }
         start_sessions(p, c, n, dstart, cnt);
         cnt.flush<M_D>();
+        c.clk.mark(PH_D);
 
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
         uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
@@ -760,14 +790,12 @@ struct Stepper {
             cnt.flush<M_A>();
         }
 
+        c.clk.mark(PH_A);
         // ---------------- C: client commands (S-11) ----------------
-        const KernArgs kp = kernargs();
-        const uint64_t cthr = kp->cmd_thr32;
-        if (cthr) {
-            const int32_t climit = kp->cmd_limit;
+        if (cmd_thr) {
             const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
-            if ((climit == 0 || n.cmdc < climit) && hw1 < cthr && lead) {
-                const bool tgt = kp->cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
+            if ((cmd_limit == 0 || n.cmdc < cmd_limit) && hw1 < cmd_thr && lead) {
+                const bool tgt = cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
                                                                       : ((lead >> r) & 1u) != 0;
                 append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
                 n.cmdc++;
@@ -775,6 +803,7 @@ struct Stepper {
             cnt.flush<M_C>();
         }
 
+        c.clk.mark(PH_C);
         // ---------------- K: end-of-step observations ----------------
         {
             const bool isl = n.role == RAFT_LEADER;
@@ -794,6 +823,7 @@ struct Stepper {
             cnt.flush<M_K>();
         }
 
+        c.clk.mark(PH_K);
         // the deferred ResettableCountdownTimer draws of this step (S-9)
         if (__ballot((n.fl & FL_DRAW) != 0)) {
             const uint32_t w = timer_word(p, c);
