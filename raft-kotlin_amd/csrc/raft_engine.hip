@@ -175,6 +175,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.iso = -1;
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
+    c.tw = c.dwt = c.dwv = 0u;
 
     Node n;
     c.clk.start();

@@ -205,12 +205,22 @@ __device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, En
     wrote = act && !overflow;
     // the one slot the new tail cache needs from HBM
     const bool ld = wrote && (ghost || (!app && i >= 1 && i != last - 1));
-    uint2 g = make_uint2(0u, 0u);
-    if (ld) g = lr[app ? last : i - 1];
+    // the new tail cache without HBM (every value but the loaded slot's)
+    int32_t t1 = e.term;
+    uint32_t c1 = e.cmd;
+    int32_t t2 = app ? n.t1 : (i == 0 ? 0 : n.t2);
+    // rare: the slot is read only if some lane of the wave needs it, and its
+    // value is consumed inside the branch, so the wave waits (vmcnt, which
+    // also counts its earlier log stores) only when a load was issued
+    if (__ballot(ld)) {
+        if (ld) {
+            const uint2 g = lr[app ? last : i - 1];
+            t1 = app ? (int32_t)g.x : t1;                   // ghost: log[last] is the new last entry
+            c1 = app ? g.y : c1;
+            t2 = app ? t2 : (int32_t)g.x;                   // overwrite: log[i-1] becomes second-to-last
+        }
+    }
     if (wrote) lr[app ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
-    const int32_t t1 = app ? (ghost ? (int32_t)g.x : e.term) : e.term;
-    const uint32_t c1 = app ? (ghost ? g.y : e.cmd) : e.cmd;
-    const int32_t t2 = app ? n.t1 : (i == 0 ? 0 : (i == last - 1 ? n.t2 : (int32_t)g.x));
     n.t1 = wrote ? t1 : n.t1;
     n.c1 = wrote ? c1 : n.c1;
     n.t2 = wrote ? t2 : n.t2;
@@ -331,7 +341,8 @@ struct Ctx {
     int iso;                  // isolated replica this step, -1 if none
     uint32_t part;            // replicas on side B of this step's partition
     uint2* lr;                // this replica's log
-    u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS)
+    u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
+    uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
 
@@ -376,20 +387,27 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int 
 
 template <int R, bool HAVE_JOB>
 __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s,
-                                              int first_job, int s_job) {
+                                              uint32_t prefetched, int s_job) {
     if (p.drop_thr16 == 0) return 0u;
     uint32_t w = 0;
     bool need = true;
     if constexpr (HAVE_JOB) {
-        const int dd = c.r < s ? c.r : c.r - 1;
-        const int q = dd < 0 ? 0 : dd;
-        w = job_word(c, first_job + (q >> 2), q & 3);
+        w = prefetched;
         need = s != s_job;
     }
     if (__ballot(need)) {
         if (need) w = drop_word_direct(p, c, purpose, s);
     }
     return w;
+}
+
+// This lane's word of the drop-word chunks the step's jobs drew for sender s
+// (first_job = J_TICK / J_VOTE).  MUST be called in group-uniform control flow.
+template <int R>
+__device__ __forceinline__ uint32_t job_drop_word(const Ctx<R>& c, int first_job, int s) {
+    const int dd = c.r < s ? c.r : c.r - 1;
+    const int q = dd < 0 ? 0 : dd;
+    return job_word(c, first_job + (q >> 2), q & 3);
 }
 
 // The step's per-replica draw word, word r & 3 of Philox(t, gid, TIMER, r >> 2)
@@ -399,7 +417,7 @@ __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& 
 template <int R>
 __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>& c) {
     if constexpr (Lanes<R>::JOBS) {
-        return job_word(c, Lanes<R>::J_TIMER + (c.r >> 2), c.r & 3);
+        return c.tw;
     } else {
         return word_of(draw(p, c.t, c.gid, RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
     }
@@ -480,7 +498,13 @@ struct Stepper {
     // destinations at once; responses are replayed in destination order.
     __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, int s, Counters& cnt) {
         const int sl = c.src(s);
+        // the leader's tick-start snapshot and this destination's drop word,
+        // all cross-lane reads issued together (one LDS round trip)
         const int32_t role_s = bcast(n.role, sl);
+        const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
+        const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
+        const uint32_t Lc1 = bcastu(n.c1, sl);
+        const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, s, c.dwt, c.s_tick);
         if (role_s == RAFT_FOLLOWER) {                                    // :117 cancel() (S-10)
             if (c.r == s) n.fl &= ~FL_HB;
             return;
@@ -491,10 +515,6 @@ struct Stepper {
             spill_load(p, c, n, s);
             n.s0 = s;
         }
-        const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
-        const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
-        const uint32_t Lc1 = bcastu(n.c1, sl);
-
         // build this destination's request (RaftServer.kt:122-132)
         const int32_t i = n.nx, prev = i - 2;
         const bool pv = prev >= 0;
@@ -518,11 +538,13 @@ struct Stepper {
         const bool ld1 = ok && prev >= 0 && !h1;
         const bool ld2 = ok && has && i != Llast;
         const bool ld3 = ok && prev >= 0 && prev < n.last && !h2;
-        if (ld1) lpt = (int32_t)ls[prev].x;
-        if (ld2) lent = ls[i - 1];
-        if (ld3) dpt = (int32_t)c.lr[prev].x;
+        if (__ballot(ld1 || ld2 || ld3)) {                                // rare: tail-cache misses
+            if (ld1) lpt = (int32_t)ls[prev].x;
+            if (ld2) lent = ls[i - 1];
+            if (ld3) dpt = (int32_t)c.lr[prev].x;
+            asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt));   // wait inside the branch
+        }
 
-        const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, s, L::J_TICK, c.s_tick);
         cnt.add_if(ok, RAFT_C_APPEND_SENT);
         const bool lreq = ok && lost(p, c, s, c.r, dw, 0);                // :170-172
         const bool act = ok && !lreq;
@@ -594,7 +616,7 @@ struct Stepper {
         const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
-        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, L::J_VOTE, c.s_vote);
+        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, c.dwv, c.s_vote);
         const bool mine = (ms >> r) & 1u;
         const bool lreq = mine && lost(p, c, s, r, dw, 0);          // retry{} swallows, Commons.kt:41
         const bool act = mine && !lreq;
@@ -706,6 +728,10 @@ struct Stepper {
             hw0 = bcastu(c.job.x, c.base);
             hw1 = bcastu(c.job.y, c.base);
             hw2 = bcastu(c.job.z, c.base);
+            // every word this lane needs from the jobs, fetched in one batch
+            c.tw = job_word(c, L::J_TIMER + (r >> 2), r & 3);
+            if constexpr (L::TICK_JOB) c.dwt = job_drop_word(c, L::J_TICK, c.s_tick);
+            if constexpr (L::VOTE_JOB) c.dwv = job_drop_word(c, L::J_VOTE, c.s_vote);
         } else {
             const u32x4 h = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
             hw0 = h.x; hw1 = h.y; hw2 = h.z;
