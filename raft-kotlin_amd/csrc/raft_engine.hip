@@ -169,9 +169,10 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.r = r;
     c.base = j * R;
     c.live = live;
-    c.idx = g * R + r;
-    c.gid = (uint32_t)(p.g0 + g);
-    c.lr = p.log + (live ? c.idx : 0) * (int64_t)p.cap;
+    c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
+    c.gg0 = (uint32_t)(p.g0 + c.wg0);
+    const int64_t idx = g * R + r;
+    c.lr = p.log + (live ? idx : 0) * (int64_t)p.cap;
     c.iso = -1;
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
@@ -179,7 +180,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
 
     Node n;
     c.clk.start();
-    if (live) load_node(n, p, g, c.idx);
+    if (live) load_node(n, p, g, idx);
     else inert_node(n);
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;
@@ -194,7 +195,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         if (pperiod > 0) {                                                // S-11 partitions
             const uint32_t ph = t % (uint32_t)pperiod;
             if ((int64_t)ph < kp->part_len) {
-                if (k == 0 || ph == 0) c.part = draw(p, t - ph, c.gid, RAFT_RNG_PARTITION, 0).x & L::ALL;
+                if (k == 0 || ph == 0) c.part = draw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
             } else {
                 c.part = 0;
             }
@@ -225,7 +226,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         const KernArgs kp = kernargs();            // state pointers re-read, not kept live across the loop
         DevParams q;
         q.st = kp->st; q.ses = kp->ses; q.gx = kp->gx; q.GR = kp->GR; q.G = kp->G;
-        store_node(n, q, g, c.idx, r == 0);
+        store_node(n, q, g, c.idx(), r == 0);
     }
 }
 

@@ -334,10 +334,10 @@ struct Lanes {
 // Per-lane, per-step context.
 template <int R>
 struct Ctx {
-    uint32_t t, gid;
+    uint32_t t;
+    uint32_t wg0, gg0;        // wave-uniform: engine-local / global id of the wave's first group
     int r, base;              // replica index, first lane of the group
     bool live;                // lane holds a real replica (whole groups are live or not)
-    int64_t idx;              // g * R + r
     int iso;                  // isolated replica this step, -1 if none
     uint32_t part;            // replicas on side B of this step's partition
     uint2* lr;                // this replica's log
@@ -350,6 +350,12 @@ struct Ctx {
         return (uint32_t)(b >> base) & Lanes<R>::ALL;
     }
     __device__ __forceinline__ int src(int s) const { return base + s; }
+    // derived on demand instead of held in VGPRs (register pressure)
+    __device__ __forceinline__ uint32_t j() const {                 // group within the wave: base / R
+        return ((uint32_t)base * ((65536u + R - 1) / R)) >> 16;
+    }
+    __device__ __forceinline__ uint32_t gid() const { return gg0 + j(); }          // global group id
+    __device__ __forceinline__ int64_t idx() const { return (int64_t)wg0 * R + base + r; }   // g * R + r
 };
 
 template <int R>
@@ -369,11 +375,11 @@ __device__ __forceinline__ bool lost(const DevParams& p, const Ctx<R>& c, int s,
 template <int R>
 __device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s) {
 #ifdef RAFT_EXP_CHEAP_DROP
-    return (c.gid * 0x9E3779B1u) ^ (c.t * 0x85EBCA6Bu) ^ ((uint32_t)s << 13) ^ ((uint32_t)c.r << 7);
+    return (c.gid() * 0x9E3779B1u) ^ (c.t * 0x85EBCA6Bu) ^ ((uint32_t)s << 13) ^ ((uint32_t)c.r << 7);
 #endif
     const int dd = c.r < s ? c.r : c.r - 1;
     const int q = dd < 0 ? 0 : dd;
-    const u32x4 w = draw(p, c.t, c.gid, purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
+    const u32x4 w = draw(p, c.t, c.gid(), purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
     return word_of(w, q & 3);
 }
 
@@ -419,7 +425,7 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
     if constexpr (Lanes<R>::JOBS) {
         return c.tw;
     } else {
-        return word_of(draw(p, c.t, c.gid, RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
+        return word_of(draw(p, c.t, c.gid(), RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
     }
 }
 
@@ -448,14 +454,14 @@ struct Stepper {
     __device__ __forceinline__ static void spill_store(const DevParams&, const Ctx<R>& c, const Node& n, int s) {
         const KernArgs kp = kernargs();
         int32_t* sp = kp->spill;
-        sp[c.idx * R + s] = n.nx;
-        sp[kp->GR * R + c.idx * R + s] = n.mc;
+        sp[c.idx() * R + s] = n.nx;
+        sp[kp->GR * R + c.idx() * R + s] = n.mc;
     }
     __device__ __forceinline__ static void spill_load(const DevParams&, const Ctx<R>& c, Node& n, int s) {
         const KernArgs kp = kernargs();
         const int32_t* sp = kp->spill;
-        n.nx = sp[c.idx * R + s];
-        n.mc = sp[kp->GR * R + c.idx * R + s];
+        n.nx = sp[c.idx() * R + s];
+        n.mc = sp[kp->GR * R + c.idx() * R + s];
     }
 
     // The flags after leaderElection() returns (S-5): the queued FOLLOWER
@@ -721,9 +727,9 @@ struct Stepper {
                 purpose = RAFT_RNG_VOTE_DROP; sub = (uint32_t)(c.s_vote & 0xFF) | ((uint32_t)(r - L::J_VOTE) << 8);
             }
 #ifdef RAFT_EXP_CHEAP_JOB
-            c.job = u32x4{c.gid * 0x9E3779B1u ^ c.t, c.t * 0x85EBCA6Bu ^ sub, purpose ^ c.gid, c.gid + c.t};
+            c.job = u32x4{c.gid() * 0x9E3779B1u ^ c.t, c.t * 0x85EBCA6Bu ^ sub, purpose ^ c.gid(), c.gid() + c.t};
 #else
-            c.job = draw(p, c.t, c.gid, purpose, sub);
+            c.job = draw(p, c.t, c.gid(), purpose, sub);
 #endif
             hw0 = bcastu(c.job.x, c.base);
             hw1 = bcastu(c.job.y, c.base);
@@ -733,13 +739,13 @@ struct Stepper {
             if constexpr (L::TICK_JOB) c.dwt = job_drop_word(c, L::J_TICK, c.s_tick);
             if constexpr (L::VOTE_JOB) c.dwv = job_drop_word(c, L::J_VOTE, c.s_vote);
         } else {
-            const u32x4 h = draw(p, c.t, c.gid, RAFT_RNG_HARNESS, 0);
+            const u32x4 h = draw(p, c.t, c.gid(), RAFT_RNG_HARNESS, 0);
             hw0 = h.x; hw1 = h.y; hw2 = h.z;
         }
 
 #ifdef RAFT_EXP_EXTRA_PHILOX
         {   // timing experiment only: one more Philox pass of the wave
-            const u32x4 x = draw(p, c.t ^ 0x5A5A5A5Au, c.gid, 77u, (uint32_t)r);
+            const u32x4 x = draw(p, c.t ^ 0x5A5A5A5Au, c.gid(), 77u, (uint32_t)r);
             if (x.x == 0x12345678u && x.y == 0x9ABCDEF0u && x.z == 1u) cnt.add(RAFT_C_LEADERS);
         }
 #endif
