@@ -420,8 +420,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
     load_rep(x, p, idx);
     uint2* lr = p.log + idx * (int64_t)p.cap;
     derive_cache(x, lr);
-    Counters cnt;
-    cnt.clear();
+    NoCounters cnt;
     for (int64_t m = off[k]; m < off[k + 1]; ++m) {
         const int64_t o = order[m];
         if (kind == BATCH_VOTE) {

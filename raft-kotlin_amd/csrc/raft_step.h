@@ -99,38 +99,30 @@ __device__ __forceinline__ KernArgs kernargs() {
     return kp;
 }
 
-// Step counters.  A handler marks an event in its lane's bit mask `ev` (bit
-// c = counter c; every counter fires at most once per lane between two
-// flushes).  flush<MASK>() -- called at wave-uniform points -- adds
-// popcount(ballot(bit c)) into the wave-uniform (SGPR) totals `s`, two 16-bit
-// counters per word (a wave's count per step is < 2^16), and clears `ev`.
-#define CBIT(c) (1u << (c))
+// Step counters of a wave.  add_if(cond, c) adds popcount(ballot(cond)) into
+// the wave-uniform (SGPR) total of counter c, two 16-bit counters per word (a
+// wave's count per step is < 2^16).  A condition is already a lane mask, so an
+// event costs a few scalar instructions and no VALU.  add_if MUST run in
+// wave-uniform control flow (the step is written branch-free for this): in a
+// divergent branch the totals would become per-lane values.
 struct Counters {
-    uint32_t ev;
     uint32_t s[NCW];
     __device__ __forceinline__ void clear() {
-        ev = 0;
 #pragma unroll
         for (int i = 0; i < NCW; ++i) s[i] = 0;
     }
 #ifdef RAFT_EXP_NO_COUNTERS
-    __device__ __forceinline__ void add(int) {}
     __device__ __forceinline__ void add_if(bool, int) {}
 #else
-    __device__ __forceinline__ void add(int c) { ev |= 1u << c; }
-    __device__ __forceinline__ void add_if(bool cond, int c) { ev |= (uint32_t)cond << c; }
-#endif
-    template <uint32_t MASK>
-    __device__ __forceinline__ void flush() {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            if ((MASK >> c) & 1u) {
-                const uint32_t k = (uint32_t)__popcll(__ballot((ev >> c) & 1u));
-                s[c >> 1] += k << (16 * (c & 1));
-            }
-        }
-        ev = 0;
+    __device__ __forceinline__ void add_if(bool cond, int c) {
+        s[c >> 1] += (uint32_t)__popcll(__ballot(cond)) << (16 * (c & 1));
     }
+#endif
+};
+// The per-message handlers of batch_kernel run in divergent control flow and
+// report no counters.
+struct NoCounters {
+    __device__ __forceinline__ void add_if(bool, int) {}
 };
 
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
@@ -229,8 +221,9 @@ __device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, En
 }
 
 // ---- vote() (RaftServer.kt:228-251), applied iff act ----------------------
+template <class CNT>
 __device__ __forceinline__ void vote_handler(Rep n, bool act, int32_t rt, int32_t rc, int32_t rli, int32_t rlt,
-                                             Counters& cnt, int32_t& resp_term, bool& granted) {
+                                             CNT& cnt, int32_t& resp_term, bool& granted) {
     const bool higher = rt > n.term;                                            // :229-231
     const bool hasl = n.last >= 1;
     const bool logrej = hasl && (rlt < n.t1 || (rlt == n.t1 && rli < n.last));  // :232-236 (Q5)
@@ -249,9 +242,10 @@ __device__ __forceinline__ void vote_handler(Rep n, bool act, int32_t rt, int32_
 // Returns false where the reference throws (Log.get with prevLogIndex < -1):
 // that call has no response.  dprev = term of this replica's log[prev], read
 // by the caller ahead of time (valid whenever 0 <= prev < lastIndex).
+template <class CNT>
 __device__ __forceinline__ bool append_handler(Rep n, bool act, int32_t id, uint2* lr, int cap, int32_t rt,
                                                int32_t rlead, int32_t prev, int32_t prevTerm, bool has, Entry e,
-                                               int32_t lcommit, int32_t dprev, Counters& cnt, int32_t& resp_term,
+                                               int32_t lcommit, int32_t dprev, CNT& cnt, int32_t& resp_term,
                                                bool& success) {
     const bool up = act && rt > n.term;                                         // :257-262
     const bool fol = up || (act && rlead != id);                                // :264-268 (Q3)
@@ -276,7 +270,8 @@ __device__ __forceinline__ bool append_handler(Rep n, bool act, int32_t id, uint
 }
 
 // ---- appendCommand() (RaftServer.kt:100-107), applied iff act -------------
-__device__ __forceinline__ void append_command(Rep n, bool act, uint2* lr, int cap, uint32_t cmd, Counters& cnt) {
+template <class CNT>
+__device__ __forceinline__ void append_command(Rep n, bool act, uint2* lr, int cap, uint32_t cmd, CNT& cnt) {
     bool wrote, ovf;
     log_add(lr, cap, n, n.last, Entry{n.term, cmd}, act, wrote, ovf);
     cnt.add_if(act, RAFT_C_COMMANDS);
@@ -371,7 +366,8 @@ __device__ __forceinline__ bool lost(const DevParams& p, const Ctx<R>& c, int s,
 // drop_word_direct evaluates it in this lane (one Philox pass serves every
 // destination of the wave); drop_word takes it from the step's jobs when they
 // hold sender s (first_job = J_TICK / J_VOTE), else draws it directly.
-// drop_word MUST be called in group-uniform control flow.
+// drop_word draws only for groups with `act`, and MUST be called in
+// group-uniform control flow.
 template <int R>
 __device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s) {
 #ifdef RAFT_EXP_CHEAP_DROP
@@ -392,14 +388,14 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int 
 }
 
 template <int R, bool HAVE_JOB>
-__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s,
-                                              uint32_t prefetched, int s_job) {
+__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, bool act,
+                                              int s, uint32_t prefetched, int s_job) {
     if (p.drop_thr16 == 0) return 0u;
     uint32_t w = 0;
-    bool need = true;
+    bool need = act;
     if constexpr (HAVE_JOB) {
         w = prefetched;
-        need = s != s_job;
+        need = act && s != s_job;
     }
     if (__ballot(need)) {
         if (need) w = drop_word_direct(p, c, purpose, s);
@@ -432,19 +428,6 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
 template <int R>
 struct Stepper {
     using L = Lanes<R>;
-    static constexpr uint32_t M_T = CBIT(RAFT_C_TIMEOUTS) | CBIT(RAFT_C_ROUNDS) | CBIT(RAFT_C_VOTE_LOG_READS) |
-                                    CBIT(RAFT_C_LEADERS_ELECTED);
-    static constexpr uint32_t M_V = CBIT(RAFT_C_MSG_DROPPED) | CBIT(RAFT_C_VOTE_LOG_READS) | CBIT(RAFT_C_VOTES_GRANTED);
-    static constexpr uint32_t M_D = CBIT(RAFT_C_LEADERS_ELECTED);
-    static constexpr uint32_t M_A = CBIT(RAFT_C_SESSIONS_TICKED) | CBIT(RAFT_C_PREV_READS_LEADER) |
-                                    CBIT(RAFT_C_ENTRY_READS_LEADER) | CBIT(RAFT_C_APPEND_SKIPPED) |
-                                    CBIT(RAFT_C_APPEND_SENT) | CBIT(RAFT_C_MSG_DROPPED) |
-                                    CBIT(RAFT_C_COMMIT_REGRESSIONS) | CBIT(RAFT_C_PREV_READS_FOLLOWER) |
-                                    CBIT(RAFT_C_ENTRY_WRITES) | CBIT(RAFT_C_LOG_OVERFLOW) |
-                                    CBIT(RAFT_C_ENTRIES_ACKED) | CBIT(RAFT_C_COMMITS);
-    static constexpr uint32_t M_C = CBIT(RAFT_C_COMMANDS) | CBIT(RAFT_C_LOG_OVERFLOW);
-    static constexpr uint32_t M_K = CBIT(RAFT_C_LEADERS) | CBIT(RAFT_C_GROUPS_WITH_LEADER) |
-                                    CBIT(RAFT_C_DUAL_LEADER_GROUPS);
     static constexpr int MAJ = L::MAJ;
     static constexpr uint32_t ALL = L::ALL;
 
@@ -483,26 +466,30 @@ struct Stepper {
                                                           Counters& cnt) {
         const uint64_t b = __ballot(starting);
         if (b == 0) return;
-        if (starting) cnt.add(RAFT_C_LEADERS_ELECTED);
+        cnt.add_if(starting, RAFT_C_LEADERS_ELECTED);
         const uint32_t sb = c.gbits(b);
 #pragma unroll
         for (int s = 0; s < R; ++s) {
             if (!(b & L::lanes_of(s))) continue;                          // wave-uniform
             const int32_t cs = bcast(n.commit, c.src(s));
-            if ((sb >> s) & 1u) {                                         // group-uniform
-                if (n.s0 >= 0 && n.s0 != s) spill_store(p, c, n, n.s0);
-                n.s0 = s;
-                n.nx = cs + 1;                                            // :112
-                n.mc = 0;                                                 // :113
+            const bool st = (sb >> s) & 1u;
+            const bool sp = st && n.s0 >= 0 && n.s0 != s;
+            if (__ballot(sp)) {
+                if (sp) spill_store(p, c, n, n.s0);
             }
+            n.s0 = st ? s : n.s0;
+            n.nx = st ? cs + 1 : n.nx;                                    // :112
+            n.mc = st ? 0 : n.mc;                                         // :113
         }
     }
 
     // One fixedRateTimer tick of leader s (RaftServer.kt:115-176) in every
-    // group of the active lanes (group-uniform s, runtime).  Requests are built
-    // from the leader's tick-start snapshot (S-4) and delivered to all
-    // destinations at once; responses are replayed in destination order.
-    __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, int s, Counters& cnt) {
+    // group with `tk` (group-uniform s, runtime; s = 0 where !tk).  Requests
+    // are built from the leader's tick-start snapshot (S-4) and delivered to
+    // all destinations at once; responses are replayed in destination order.
+    // Predicated, called in wave-uniform control flow.
+    __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, bool tk, int s,
+                                                Counters& cnt) {
         const int sl = c.src(s);
         // the leader's tick-start snapshot and this destination's drop word,
         // all cross-lane reads issued together (one LDS round trip)
@@ -510,17 +497,20 @@ struct Stepper {
         const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
         const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
         const uint32_t Lc1 = bcastu(n.c1, sl);
-        const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, s, c.dwt, c.s_tick);
-        if (role_s == RAFT_FOLLOWER) {                                    // :117 cancel() (S-10)
-            if (c.r == s) n.fl &= ~FL_HB;
-            return;
+        const bool fol = role_s == RAFT_FOLLOWER;
+        const bool me = c.r == s;
+        const bool run = tk && !fol;
+        const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
+        n.fl &= (tk && fol && me) ? ~FL_HB : ~0u;                         // :117 cancel() (S-10)
+        cnt.add_if(run && me, RAFT_C_SESSIONS_TICKED);
+        const bool swap = run && n.s0 != s;                               // swap the session in (rare)
+        if (__ballot(swap)) {
+            if (swap) {
+                if (n.s0 >= 0) spill_store(p, c, n, n.s0);
+                spill_load(p, c, n, s);
+            }
         }
-        if (c.r == s) cnt.add(RAFT_C_SESSIONS_TICKED);
-        if (n.s0 != s) {                                                  // swap the session in
-            if (n.s0 >= 0) spill_store(p, c, n, n.s0);
-            spill_load(p, c, n, s);
-            n.s0 = s;
-        }
+        n.s0 = swap ? s : n.s0;
         // build this destination's request (RaftServer.kt:122-132)
         const int32_t i = n.nx, prev = i - 2;
         const bool pv = prev >= 0;
@@ -528,10 +518,11 @@ struct Stepper {
         const bool has_c = !pv_bad && Llast >= i;                         // :130
         const bool ent_bad = has_c && i - 1 < 0;                          // :131 throws
         const bool has = has_c && !ent_bad;
-        const bool ok = !pv_bad && !ent_bad;
-        cnt.add_if(pv && !pv_bad, RAFT_C_PREV_READS_LEADER);
-        cnt.add_if(has, RAFT_C_ENTRY_READS_LEADER);
-        cnt.add_if(!ok, RAFT_C_APPEND_SKIPPED);
+        const bool okb = !pv_bad && !ent_bad;
+        const bool ok = run && okb;
+        cnt.add_if(run && pv && !pv_bad, RAFT_C_PREV_READS_LEADER);
+        cnt.add_if(run && has, RAFT_C_ENTRY_READS_LEADER);
+        cnt.add_if(run && !okb, RAFT_C_APPEND_SKIPPED);
         // every log slot of the tick, resolved up front: the leader's log[prev]
         // and log[i-1], and this replica's own log[prev] (append() :274-276);
         // a handler only writes its own replica's log, so no handler of the
@@ -601,29 +592,30 @@ struct Stepper {
                 cnt.add_if(inc && c.r == q, RAFT_C_COMMITS);
             }
         }
-        const bool me = c.r == s;
-        const bool sd = me && stepdown;                                   // :148 + offer(FOLLOWER) :152 (S-6)
-        n.term = me ? T : n.term;
-        n.commit = me ? C : n.commit;
+        const bool wb = run && me;
+        const bool sd = wb && stepdown;                                   // :148 + offer(FOLLOWER) :152 (S-6)
+        n.term = wb ? T : n.term;
+        n.commit = wb ? C : n.commit;
         n.role = sd ? (int32_t)RAFT_FOLLOWER : n.role;
         n.fl |= (sd && !(n.fl & FL_ELECTING)) ? (FL_ARMED | FL_DRAW) : 0u;
     }
 
     // One RequestVote round: every group with a pending sender delivers the
-    // requests of its lowest remaining sender s to all destinations at once
-    // (group-uniform control flow).
+    // requests of its lowest remaining sender s to all destinations at once.
+    // Predicated, called in wave-uniform control flow.
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
                                                       uint32_t& vtodo, uint32_t send, int32_t qt, int32_t qli,
                                                       int32_t qlt) {
         const int r = c.r;
-        const int s = __builtin_ctz(vtodo);
+        const bool vr = vtodo != 0;
+        const int s = vr ? __builtin_ctz(vtodo) : 0;
         vtodo &= vtodo - 1u;
         const int sl = c.src(s);
         const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
-        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, s, c.dwv, c.s_vote);
-        const bool mine = (ms >> r) & 1u;
+        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, vr, s, c.dwv, c.s_vote);
+        const bool mine = vr && ((ms >> r) & 1u);
         const bool lreq = mine && lost(p, c, s, r, dw, 0);          // retry{} swallows, Commons.kt:41
         const bool act = mine && !lreq;
         int32_t rterm;
@@ -636,7 +628,7 @@ struct Stepper {
         const uint32_t dl = c.gbits(__ballot(delivered));
         const uint32_t gr = c.gbits(__ballot(delivered && granted));
         const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
-        const bool me = r == s;
+        const bool me = vr && r == s;
         uint32_t f = n.fl & ~(dl << PEND_SH);
         f += (uint32_t)__popc(dl) << LATCH_SH;                      // :209 countDown()
         f += (uint32_t)__popc(gr) << VOTES_SH;                      // :211
@@ -702,7 +694,6 @@ struct Stepper {
             cnt.add_if(sr, RAFT_C_ROUNDS);
         }
         start_sessions(p, c, n, sstart, cnt);
-        cnt.flush<M_T>();
         c.clk.mark(PH_T);
 
         // ---------------- the step's Philox pass (S-9) ----------------
@@ -746,7 +737,7 @@ struct Stepper {
 #ifdef RAFT_EXP_EXTRA_PHILOX
         {   // timing experiment only: one more Philox pass of the wave
             const u32x4 x = draw(p, c.t ^ 0x5A5A5A5Au, c.gid(), 77u, (uint32_t)r);
-            if (x.x == 0x12345678u && x.y == 0x9ABCDEF0u && x.z == 1u) cnt.add(RAFT_C_LEADERS);
+            cnt.add_if(x.x == 0x12345678u && x.y == 0x9ABCDEF0u && x.z == 1u, RAFT_C_LEADERS);
         }
 #endif
         c.clk.mark(PH_JOBS);
@@ -769,12 +760,9 @@ struct Stepper {
         // senders -- usually one -- with one handler per destination lane.
         uint32_t vtodo = c.gbits(__ballot(send != 0));
         if (__ballot(vtodo != 0)) {
-            if (vtodo != 0) vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);   // group-uniform
-            cnt.flush<M_V>();
-            while (__ballot(vtodo != 0)) {                                  // groups with 2+ senders (rare)
-                if (vtodo != 0) vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
-                cnt.flush<M_V>();
-            }
+            vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+            while (__ballot(vtodo != 0))                                    // groups with 2+ senders (rare)
+                vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
         }
 
         c.clk.mark(PH_V);
@@ -802,37 +790,26 @@ struct Stepper {
             if (need_bo) n.phase = scale_range(w, kp->bmin, kp->bmax);
         }
         start_sessions(p, c, n, dstart, cnt);
-        cnt.flush<M_D>();
         c.clk.mark(PH_D);
 
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
         uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
-        if (todo != 0) {                                                    // group-uniform
-            const int s = __builtin_ctz(todo);
+        while (__ballot(todo != 0)) {                                       // usually one round
+            const bool tk = todo != 0;
+            const int s = tk ? __builtin_ctz(todo) : 0;
             todo &= todo - 1u;
-            tick(p, c, n, s, cnt);
-        }
-        cnt.flush<M_A>();
-        while (__ballot(todo != 0)) {                                       // 2+ sessions (rare)
-            if (todo != 0) {
-                const int s = __builtin_ctz(todo);
-                todo &= todo - 1u;
-                tick(p, c, n, s, cnt);
-            }
-            cnt.flush<M_A>();
+            tick(p, c, n, tk, s, cnt);
         }
 
         c.clk.mark(PH_A);
         // ---------------- C: client commands (S-11) ----------------
         if (cmd_thr) {
             const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
-            if ((cmd_limit == 0 || n.cmdc < cmd_limit) && hw1 < cmd_thr && lead) {
-                const bool tgt = cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
-                                                                      : ((lead >> r) & 1u) != 0;
-                append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
-                n.cmdc++;
-            }
-            cnt.flush<M_C>();
+            const bool cm = (cmd_limit == 0 || n.cmdc < cmd_limit) && hw1 < cmd_thr && lead;
+            const bool tgt = cm && (cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
+                                                                       : ((lead >> r) & 1u) != 0);
+            append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
+            n.cmdc += cm ? 1 : 0;
         }
 
         c.clk.mark(PH_C);
@@ -840,8 +817,8 @@ struct Stepper {
         {
             const bool isl = n.role == RAFT_LEADER;
             const uint32_t lead = c.gbits(__ballot(isl));
-            if (isl) cnt.add(RAFT_C_LEADERS);
-            if (lead && r == __builtin_ctz(lead)) cnt.add(RAFT_C_GROUPS_WITH_LEADER);
+            cnt.add_if(isl, RAFT_C_LEADERS);
+            cnt.add_if(lead && r == __builtin_ctz(lead), RAFT_C_GROUPS_WITH_LEADER);
             if (__ballot(__popc(lead) >= 2)) {                              // rare
                 bool dual = false;
 #pragma unroll
@@ -850,9 +827,8 @@ struct Stepper {
                     if (isl && r < q && ((lead >> q) & 1u) && tq == n.term) dual = true;
                 }
                 const uint32_t db = c.gbits(__ballot(dual));
-                if (db && r == 0) cnt.add(RAFT_C_DUAL_LEADER_GROUPS);
+                cnt.add_if(db && r == 0, RAFT_C_DUAL_LEADER_GROUPS);
             }
-            cnt.flush<M_K>();
         }
 
         c.clk.mark(PH_K);
