@@ -182,14 +182,24 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.clk.start();
     if (live) load_node(n, p, g, idx);
     else inert_node(n);
+    // Drain the state loads here: left pending into the loop, they make the
+    // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
+    // previous step's log stores, so each step would start by waiting for them.
+    __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;
         c.t = t;
-        // Rematerialise the lane geometry every step: otherwise the optimiser
-        // hoists dozens of loop-invariant lane masks (r == 1, r < 2, ...) out
-        // of the step loop, and each one pins an SGPR pair for the whole
-        // kernel (spilled to VGPR lanes and reloaded at every use).
-        asm volatile("" : "+v"(c.r), "+v"(c.base));
+        // Re-derive the lane geometry from the lane id every step, behind an
+        // opaque copy: otherwise the optimiser hoists dozens of loop-invariant
+        // lane masks (r == 1, r < 2, ...) out of the step loop, and each one
+        // pins an SGPR pair for the whole kernel (spilled to VGPR lanes and
+        // reloaded at every use).  r and base are then dead between steps.
+        {
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            c.base = (int)(((uint32_t)ln * ((65536u + R - 1) / R)) >> 16) * R;
+            c.r = ln - c.base;
+        }
         const KernArgs kp = kernargs();
         const int32_t pperiod = kp->part_period;
         if (pperiod > 0) {                                                // S-11 partitions
@@ -206,7 +216,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         c.clk.mark(PH_TDRAW);
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
-        for (int cw = 0; cw < NCW; ++cw) v = lane == cw ? cnt.s[cw] : v;
+        for (int cw = 0; cw < NCW; ++cw) v = (uint32_t)raft_writelane((int32_t)cnt.s[cw], cw, (int32_t)v);
         if (lane < NCW) lds_cnt[(k * WAVES_PER_BLOCK + wib) * NCW + lane] = v;
         c.clk.mark(PH_CNT);
     }

@@ -38,6 +38,8 @@
 #include "../../include/raft_engine.h"
 
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
+// v_writelane_b32: one SGPR value into one lane of a VGPR
+extern "C" __device__ int32_t raft_writelane(int32_t val, int32_t lane, int32_t old) __asm("llvm.amdgcn.writelane.i32");
 
 namespace raft {
 
