@@ -647,16 +647,19 @@ struct Stepper {
         // T draws no randomness, so it runs before the step's Philox pass and
         // that pass already knows the first RequestVote sender.
         const uint32_t lead0 = c.gbits(__ballot(n.role == RAFT_LEADER));
-        // harness parameters, read at step start (kernargs()) so the scalar
-        // loads are in flight while T runs
-        const KernArgs kp = kernargs();
-        const uint64_t churn_thr = kp->churn_thr32, cmd_thr = kp->cmd_thr32;
-        const int32_t churn_steps = kp->churn_steps, cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
 
         // ---------------- T: timers and election clocks ----------------
         uint32_t send;
         int32_t qt, qli, qlt;
         bool sstart;
+        // a wave where no timer fires and no replica is electing only counts
+        // its armed timers down (most waves in steady state)
+        const bool t_armed = n.fl & FL_ARMED;
+        const int32_t t_el = n.elec - p.P;
+        if (!__ballot((n.fl & FL_ELECTING) || (t_armed && t_el <= 0))) {
+            n.elec = t_armed ? t_el : n.elec;
+            send = 0u; sstart = false; qt = qli = qlt = 0;
+        } else
         {
             uint32_t f = n.fl;
             const bool armed = f & FL_ARMED;
@@ -745,6 +748,11 @@ struct Stepper {
         c.clk.mark(PH_JOBS);
         // ---------------- H: harness ----------------
         {
+            // harness parameters re-read where used (kernargs()): held across
+            // the step they would be spilled into VGPR lanes
+            const KernArgs kp = kernargs();
+            const uint64_t churn_thr = kp->churn_thr32;
+            const int32_t churn_steps = kp->churn_steps;
             int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
             if (rem > 0) { rem--; if (rem == 0) rep = 0; }
             if (churn_thr && churn_steps > 0 && rem == 0 && hw0 < churn_thr && lead0) {
@@ -796,16 +804,29 @@ struct Stepper {
 
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
         uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
-        while (__ballot(todo != 0)) {                                       // usually one round
-            const bool tk = todo != 0;
-            const int s = tk ? __builtin_ctz(todo) : 0;
-            todo &= todo - 1u;
-            tick(p, c, n, tk, s, cnt);
+        // the first round peeled: the common case runs no loop (a loop makes
+        // the compiler carry the counters in VGPRs and copy the node per round)
+        if (__ballot(todo != 0)) {
+            {
+                const bool tk = todo != 0;
+                const int s = tk ? __builtin_ctz(todo) : 0;
+                todo &= todo - 1u;
+                tick(p, c, n, tk, s, cnt);
+            }
+            while (__ballot(todo != 0)) {                                   // 2+ sessions (rare)
+                const bool tk = todo != 0;
+                const int s = tk ? __builtin_ctz(todo) : 0;
+                todo &= todo - 1u;
+                tick(p, c, n, tk, s, cnt);
+            }
         }
 
         c.clk.mark(PH_A);
         // ---------------- C: client commands (S-11) ----------------
+        const KernArgs kp = kernargs();
+        const uint64_t cmd_thr = kp->cmd_thr32;
         if (cmd_thr) {
+            const int32_t cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
             const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
             const bool cm = (cmd_limit == 0 || n.cmdc < cmd_limit) && hw1 < cmd_thr && lead;
             const bool tgt = cm && (cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
