@@ -435,20 +435,23 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
         const int64_t o = order[m];
         if (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
-            int32_t rt; bool gr;
-            vote_handler(x.ref(), true, q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
-            ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, gr ? 1 : 0};
+            int32_t rt;
+            uint64_t gr;
+            vote_handler(x.ref(), __ballot(1), q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
+            ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
-            int32_t rt = 0; bool su = false;
+            int32_t rt = 0;
+            uint64_t su = 0;
             const int32_t pv = q.prev_log_index;
             const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lr[pv].x : 0;
-            const bool okh = append_handler(x.ref(), true, r + 1, lr, p.cap, q.term, q.leader_id, pv,
-                                            q.prev_log_term, q.has_entry != 0, Entry{q.entry_term, q.entry_cmd},
-                                            q.leader_commit, dprev, cnt, rt, su);
-            ((raft_append_resp*)resp)[o] = raft_append_resp{rt, su ? 1 : 0, okh ? 0 : 1};
+            const uint64_t thrown = append_handler(x.ref(), __ballot(1), r + 1, lr, p.cap, q.term, q.leader_id, pv,
+                                                   q.prev_log_term, __ballot(q.has_entry != 0),
+                                                   Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, cnt, rt,
+                                                   su);
+            ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
-            append_command(x.ref(), true, lr, p.cap, ((const uint32_t*)req)[o], cnt);
+            append_command(x.ref(), __ballot(1), lr, p.cap, ((const uint32_t*)req)[o], cnt);
         }
         resolve_rep_draw(x, p, t, gid, r);
     }

@@ -101,12 +101,20 @@ __device__ __forceinline__ KernArgs kernargs() {
     return kp;
 }
 
-// Step counters of a wave.  add_if(cond, c) adds popcount(ballot(cond)) into
-// the wave-uniform (SGPR) total of counter c, two 16-bit counters per word (a
-// wave's count per step is < 2^16).  A condition is already a lane mask, so an
-// event costs a few scalar instructions and no VALU.  add_if MUST run in
-// wave-uniform control flow (the step is written branch-free for this): in a
-// divergent branch the totals would become per-lane values.
+// Lane masks.  The step's predicates are built as 64-bit lane masks (SGPR
+// pairs): lm() of a single comparison is that comparison's own v_cmp result,
+// masks combine with scalar &, |, &~, and ib() turns a mask back into this
+// lane's bool for a select at no cost.  (__ballot of a composite bool such as
+// a && b would make the compiler materialise the bool in a VGPR and compare
+// it again: two VALU per ballot.)  Negations are only ever taken inside a
+// positive mask, so dead lanes (inert nodes) never satisfy a predicate.
+__device__ __forceinline__ uint64_t lm(bool cmp) { return __ballot(cmp); }
+__device__ __forceinline__ bool ib(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
+// Step counters of a wave.  add(m, c) adds popcount(m) -- the lanes where
+// counter c's event happened -- into the wave-uniform (SGPR) total of counter
+// c, two 16-bit counters per word (a wave's count per step is < 2^16).  Called
+// in wave-uniform control flow, where a lane mask covers the whole wave.
 struct Counters {
     uint32_t s[NCW];
     __device__ __forceinline__ void clear() {
@@ -114,17 +122,15 @@ struct Counters {
         for (int i = 0; i < NCW; ++i) s[i] = 0;
     }
 #ifdef RAFT_EXP_NO_COUNTERS
-    __device__ __forceinline__ void add_if(bool, int) {}
+    __device__ __forceinline__ void add(uint64_t, int) {}
 #else
-    __device__ __forceinline__ void add_if(bool cond, int c) {
-        s[c >> 1] += (uint32_t)__popcll(__ballot(cond)) << (16 * (c & 1));
-    }
+    __device__ __forceinline__ void add(uint64_t m, int c) { s[c >> 1] += (uint32_t)__popcll(m) << (16 * (c & 1)); }
 #endif
 };
 // The per-message handlers of batch_kernel run in divergent control flow and
 // report no counters.
 struct NoCounters {
-    __device__ __forceinline__ void add_if(bool, int) {}
+    __device__ __forceinline__ void add(uint64_t, int) {}
 };
 
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
@@ -170,18 +176,20 @@ __device__ __forceinline__ uint32_t follower_sent(uint32_t fl) {
     return (fl & FL_ELECTING) ? FL_PRST : (FL_ARMED | FL_DRAW);
 }
 
-// The handlers below are written as predicated selects (applied iff `act`)
-// with at most one optional load and one optional store, not as nested ifs:
-// in SIMT every branch side costs the whole wave, and branch merges cost
-// register copies.  Semantics are exactly the reference's (cited per line).
+// The handlers below are written as predicated selects (applied on the lanes
+// of the mask `act`) with at most one optional load and one optional store,
+// not as nested ifs: in SIMT every branch side costs the whole wave, and
+// branch merges cost register copies.  Their predicates are lane masks (see
+// lm()), which also work in the divergent per-message loops of batch_kernel
+// (inactive lanes are simply absent from every mask).  Semantics are exactly
+// the reference's (cited per line).
 
 // ---- Log<T> (Commons.kt:47-74) over one replica's HBM slots ---------------
 // The 2-deep tail cache answers every steady-state read (prev checks, the
 // newest entry, vote last-terms); HBM is read for older slots and when the
 // ghost tail resurfaces a stale slot.
-__device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t t2, int32_t j, bool& hit) {
-    hit = j == last - 1 || j == last - 2;
-    return j == last - 1 ? t1 : t2;
+__device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t t2, int32_t j) {
+    return j == last - 1 ? t1 : t2;                    // valid for j in {last-1, last-2}
 }
 
 // Log.add(i, e) for 0 <= i <= lastIndex, the only indices its callers pass:
@@ -190,94 +198,99 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
 //   i == lastIndex: :58-61, log.add(entry) appends at the PHYSICAL end (Q1);
 //   i <  lastIndex: :63-66, log[i] = entry, lastIndex = i + 1, no shrink.
 // The build refuses an append beyond log_cap (counted, never wrapped).
-__device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e, bool act, bool& wrote,
-                                        bool& overflow) {
+__device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
+                                        uint64_t& overflow) {
     const int32_t last = n.last, phys = n.phys;
-    const bool app = i == last;
-    const bool ghost = app && phys != last;            // the stale slot log[last] becomes the last entry
-    overflow = act && app && phys >= cap;
-    wrote = act && !overflow;
+    const uint64_t app = lm(i == last);
+    const uint64_t ghost = app & lm(phys != last);     // the stale slot log[last] becomes the last entry
+    overflow = act & app & lm(phys >= cap);
+    wrote = act & ~overflow;
     // the one slot the new tail cache needs from HBM
-    const bool ld = wrote && (ghost || (!app && i >= 1 && i != last - 1));
+    const uint64_t ld = wrote & (ghost | (lm(i != last) & lm(i >= 1) & lm(i != last - 1)));
+    const bool ap = ib(app);
     // the new tail cache without HBM (every value but the loaded slot's)
     int32_t t1 = e.term;
     uint32_t c1 = e.cmd;
-    int32_t t2 = app ? n.t1 : (i == 0 ? 0 : n.t2);
+    int32_t t2 = ap ? n.t1 : (i == 0 ? 0 : n.t2);
     // rare: the slot is read only if some lane of the wave needs it, and its
     // value is consumed inside the branch, so the wave waits (vmcnt, which
     // also counts its earlier log stores) only when a load was issued
-    if (__ballot(ld)) {
-        if (ld) {
-            const uint2 g = lr[app ? last : i - 1];
-            t1 = app ? (int32_t)g.x : t1;                   // ghost: log[last] is the new last entry
-            c1 = app ? g.y : c1;
-            t2 = app ? t2 : (int32_t)g.x;                   // overwrite: log[i-1] becomes second-to-last
+    if (ld) {
+        if (ib(ld)) {
+            const uint2 g = lr[ap ? last : i - 1];
+            t1 = ap ? (int32_t)g.x : t1;                    // ghost: log[last] is the new last entry
+            c1 = ap ? g.y : c1;
+            t2 = ap ? t2 : (int32_t)g.x;                    // overwrite: log[i-1] becomes second-to-last
         }
     }
-    if (wrote) lr[app ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
-    n.t1 = wrote ? t1 : n.t1;
-    n.c1 = wrote ? c1 : n.c1;
-    n.t2 = wrote ? t2 : n.t2;
-    n.phys = wrote && app ? phys + 1 : phys;
-    n.last = wrote ? i + 1 : last;
+    const bool w = ib(wrote);
+    if (w) lr[ap ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
+    n.t1 = w ? t1 : n.t1;
+    n.c1 = w ? c1 : n.c1;
+    n.t2 = w ? t2 : n.t2;
+    n.phys = ib(wrote & app) ? phys + 1 : phys;
+    n.last = w ? i + 1 : last;
 }
 
-// ---- vote() (RaftServer.kt:228-251), applied iff act ----------------------
+// ---- vote() (RaftServer.kt:228-251), applied on the lanes of act ----------
 template <class CNT>
-__device__ __forceinline__ void vote_handler(Rep n, bool act, int32_t rt, int32_t rc, int32_t rli, int32_t rlt,
-                                             CNT& cnt, int32_t& resp_term, bool& granted) {
-    const bool higher = rt > n.term;                                            // :229-231
-    const bool hasl = n.last >= 1;
-    const bool logrej = hasl && (rlt < n.t1 || (rlt == n.t1 && rli < n.last));  // :232-236 (Q5)
-    const bool up = act && higher && !logrej;                                   // :237-242
-    granted = up || (act && rt == n.term && n.voted == rc);                     // :230
-    cnt.add_if(act && higher && hasl, RAFT_C_VOTE_LOG_READS);
-    cnt.add_if(granted, RAFT_C_VOTES_GRANTED);
-    n.fl |= up ? follower_sent(n.fl) : 0u;                                      // :241
-    n.term = up ? rt : n.term;
-    n.voted = up ? rc : n.voted;
-    n.role = up ? (int32_t)RAFT_FOLLOWER : n.role;
+__device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t rt, int32_t rc, int32_t rli, int32_t rlt,
+                                             CNT& cnt, int32_t& resp_term, uint64_t& granted) {
+    const uint64_t higher = lm(rt > n.term);                                    // :229-231
+    const uint64_t hasl = lm(n.last >= 1);
+    const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));   // :232-236 (Q5)
+    const uint64_t up = act & higher & ~logrej;                                 // :237-242
+    granted = up | (act & lm(rt == n.term) & lm(n.voted == rc));                // :230
+    cnt.add(act & higher & hasl, RAFT_C_VOTE_LOG_READS);
+    cnt.add(granted, RAFT_C_VOTES_GRANTED);
+    const bool u = ib(up);
+    n.fl |= u ? follower_sent(n.fl) : 0u;                                       // :241
+    n.term = u ? rt : n.term;
+    n.voted = u ? rc : n.voted;
+    n.role = u ? (int32_t)RAFT_FOLLOWER : n.role;
     resp_term = n.term;                                                         // :246-249
 }
 
-// ---- append() (RaftServer.kt:253-287), applied iff act --------------------
-// Returns false where the reference throws (Log.get with prevLogIndex < -1):
-// that call has no response.  dprev = term of this replica's log[prev], read
-// by the caller ahead of time (valid whenever 0 <= prev < lastIndex).
+// ---- append() (RaftServer.kt:253-287), applied on the lanes of act --------
+// Returns the lanes where the reference throws (Log.get with prevLogIndex <
+// -1): those calls have no response.  dprev = term of this replica's
+// log[prev], read by the caller ahead of time (valid whenever 0 <= prev <
+// lastIndex).
 template <class CNT>
-__device__ __forceinline__ bool append_handler(Rep n, bool act, int32_t id, uint2* lr, int cap, int32_t rt,
-                                               int32_t rlead, int32_t prev, int32_t prevTerm, bool has, Entry e,
-                                               int32_t lcommit, int32_t dprev, CNT& cnt, int32_t& resp_term,
-                                               bool& success) {
-    const bool up = act && rt > n.term;                                         // :257-262
-    const bool fol = up || (act && rlead != id);                                // :264-268 (Q3)
-    n.fl |= fol ? follower_sent(n.fl) : 0u;
-    n.term = up ? rt : n.term;
-    n.voted = up ? -1 : n.voted;
-    n.role = fol ? (int32_t)RAFT_FOLLOWER : n.role;
-    const bool cu = act && lcommit > n.commit;                                  // :270-272 (Q4)
+__device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, uint2* lr, int cap, int32_t rt,
+                                                   int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
+                                                   Entry e, int32_t lcommit, int32_t dprev, CNT& cnt,
+                                                   int32_t& resp_term, uint64_t& success) {
+    const uint64_t up = act & lm(rt > n.term);                                  // :257-262
+    const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
+    const bool u = ib(up), f = ib(fol);
+    n.fl |= f ? follower_sent(n.fl) : 0u;
+    n.term = u ? rt : n.term;
+    n.voted = u ? -1 : n.voted;
+    n.role = f ? (int32_t)RAFT_FOLLOWER : n.role;
+    const uint64_t cu = act & lm(lcommit > n.commit);                           // :270-272 (Q4)
     const int32_t cc = min(lcommit, n.last);
-    cnt.add_if(cu && cc < n.commit, RAFT_C_COMMIT_REGRESSIONS);
-    n.commit = cu ? cc : n.commit;
-    const bool check = prev != -1 && n.last > prev;                             // :274-276
-    const bool thrown = check && prev < 0;
-    cnt.add_if(act && check && !thrown, RAFT_C_PREV_READS_FOLLOWER);
-    success = act && (prev == -1 || (check && !thrown && dprev == prevTerm));
-    bool wrote, ovf;
-    log_add(lr, cap, n, prev + 1, e, success && has, wrote, ovf);               // :278 (Q2, Q10)
-    cnt.add_if(wrote, RAFT_C_ENTRY_WRITES);
-    cnt.add_if(ovf, RAFT_C_LOG_OVERFLOW);
+    cnt.add(cu & lm(cc < n.commit), RAFT_C_COMMIT_REGRESSIONS);
+    n.commit = ib(cu) ? cc : n.commit;
+    const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
+    const uint64_t thrown = check & lm(prev < 0);
+    cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
+    success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
+    uint64_t wrote, ovf;
+    log_add(lr, cap, n, prev + 1, e, success & has, wrote, ovf);                // :278 (Q2, Q10)
+    cnt.add(wrote, RAFT_C_ENTRY_WRITES);
+    cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
     resp_term = n.term;                                                         // :282-285
-    return !thrown;
+    return thrown;
 }
 
-// ---- appendCommand() (RaftServer.kt:100-107), applied iff act -------------
+// ---- appendCommand() (RaftServer.kt:100-107), applied on the lanes of act -
 template <class CNT>
-__device__ __forceinline__ void append_command(Rep n, bool act, uint2* lr, int cap, uint32_t cmd, CNT& cnt) {
-    bool wrote, ovf;
+__device__ __forceinline__ void append_command(Rep n, uint64_t act, uint2* lr, int cap, uint32_t cmd, CNT& cnt) {
+    uint64_t wrote, ovf;
     log_add(lr, cap, n, n.last, Entry{n.term, cmd}, act, wrote, ovf);
-    cnt.add_if(act, RAFT_C_COMMANDS);
-    cnt.add_if(ovf, RAFT_C_LOG_OVERFLOW);
+    cnt.add(act, RAFT_C_COMMANDS);
+    cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
 }
 
 // ---------------------------------------------------------------------------
@@ -355,12 +368,13 @@ struct Ctx {
     __device__ __forceinline__ int64_t idx() const { return (int64_t)wg0 * R + base + r; }   // g * R + r
 };
 
+// The lanes whose message s -> d is lost (S-7): churn isolation, partition
+// sides, or the drop uniform j = 2*dd + b (word dd, half b); self never lost.
 template <int R>
-__device__ __forceinline__ bool lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
-    const bool iso = c.iso >= 0 && (s == c.iso || d == c.iso);                 // churn isolation
-    const bool part = ((c.part >> s) ^ (c.part >> d)) & 1u;                     // partition sides
-    const bool drop = ((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16;              // uniform j = 2*dd + b: word dd, half b
-    return s != d && (iso || part || drop);                                     // S-7: self never lost
+__device__ __forceinline__ uint64_t lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
+    const uint64_t net = lm(s == c.iso) | lm(d == c.iso) |                      // iso = -1: nobody isolated
+                         lm(((c.part >> s) ^ (c.part >> d)) & 1u);
+    return lm(s != d) & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
 }
 
 // 16-bit drop uniforms of sender s for this lane as destination d (S-9):
@@ -390,17 +404,17 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int 
 }
 
 template <int R, bool HAVE_JOB>
-__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, bool act,
+__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, uint64_t act,
                                               int s, uint32_t prefetched, int s_job) {
     if (p.drop_thr16 == 0) return 0u;
     uint32_t w = 0;
-    bool need = act;
+    uint64_t need = act;
     if constexpr (HAVE_JOB) {
         w = prefetched;
-        need = act && s != s_job;
+        need = act & lm(s != s_job);
     }
-    if (__ballot(need)) {
-        if (need) w = drop_word_direct(p, c, purpose, s);
+    if (need) {
+        if (ib(need)) w = drop_word_direct(p, c, purpose, s);
     }
     return w;
 }
@@ -461,24 +475,24 @@ struct Stepper {
     }
 
     // appendRequestAndLeaderHeartbeat() entry (RaftServer.kt:109-113) for every
-    // lane with `starting`, in ascending replica order within a group: each
+    // lane of `starting`, in ascending replica order within a group: each
     // start takes over the primary slot, the previous owner's row goes to spill.
     // Called in wave-uniform control flow.
-    __device__ __forceinline__ static void start_sessions(const DevParams& p, const Ctx<R>& c, Node& n, bool starting,
+    __device__ __forceinline__ static void start_sessions(const DevParams& p, const Ctx<R>& c, Node& n, uint64_t starting,
                                                           Counters& cnt) {
-        const uint64_t b = __ballot(starting);
-        if (b == 0) return;
-        cnt.add_if(starting, RAFT_C_LEADERS_ELECTED);
-        const uint32_t sb = c.gbits(b);
+        if (starting == 0) return;
+        cnt.add(starting, RAFT_C_LEADERS_ELECTED);
+        const uint32_t sb = c.gbits(starting);
 #pragma unroll
         for (int s = 0; s < R; ++s) {
-            if (!(b & L::lanes_of(s))) continue;                          // wave-uniform
+            if (!(starting & L::lanes_of(s))) continue;                   // wave-uniform
             const int32_t cs = bcast(n.commit, c.src(s));
-            const bool st = (sb >> s) & 1u;
-            const bool sp = st && n.s0 >= 0 && n.s0 != s;
-            if (__ballot(sp)) {
-                if (sp) spill_store(p, c, n, n.s0);
+            const uint64_t mst = lm((sb >> s) & 1u);
+            const uint64_t msp = mst & lm(n.s0 >= 0) & lm(n.s0 != s);
+            if (msp) {
+                if (ib(msp)) spill_store(p, c, n, n.s0);
             }
+            const bool st = ib(mst);
             n.s0 = st ? s : n.s0;
             n.nx = st ? cs + 1 : n.nx;                                    // :112
             n.mc = st ? 0 : n.mc;                                         // :113
@@ -499,102 +513,104 @@ struct Stepper {
         const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
         const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
         const uint32_t Lc1 = bcastu(n.c1, sl);
-        const bool fol = role_s == RAFT_FOLLOWER;
-        const bool me = c.r == s;
-        const bool run = tk && !fol;
+        const uint64_t mtk = lm(tk), mme = lm(c.r == s);
+        const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
         const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
-        n.fl &= (tk && fol && me) ? ~FL_HB : ~0u;                         // :117 cancel() (S-10)
-        cnt.add_if(run && me, RAFT_C_SESSIONS_TICKED);
-        const bool swap = run && n.s0 != s;                               // swap the session in (rare)
-        if (__ballot(swap)) {
-            if (swap) {
+        n.fl &= ib(mtk & ~run & mme) ? ~FL_HB : ~0u;                      // :117 cancel() (S-10)
+        cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
+        const uint64_t swap = run & lm(n.s0 != s);                        // swap the session in (rare)
+        if (swap) {
+            if (ib(swap)) {
                 if (n.s0 >= 0) spill_store(p, c, n, n.s0);
                 spill_load(p, c, n, s);
             }
         }
-        n.s0 = swap ? s : n.s0;
-        // build this destination's request (RaftServer.kt:122-132)
+        n.s0 = ib(swap) ? s : n.s0;
+        // build this destination's request (RaftServer.kt:122-132).  With
+        // prev = i - 2: Log.get(prev) throws for prev > lastIndex - 1 (:128,
+        // Q11) and log[i-1] for i < 1 (:131), so the request goes out iff
+        // -1 <= prev < lastIndex, and carries an entry iff also i <= lastIndex.
         const int32_t i = n.nx, prev = i - 2;
-        const bool pv = prev >= 0;
-        const bool pv_bad = pv && prev > Llast - 1;                     // :128 Log.get throws (Q11)
-        const bool has_c = !pv_bad && Llast >= i;                         // :130
-        const bool ent_bad = has_c && i - 1 < 0;                          // :131 throws
-        const bool has = has_c && !ent_bad;
-        const bool okb = !pv_bad && !ent_bad;
-        const bool ok = run && okb;
-        cnt.add_if(run && pv && !pv_bad, RAFT_C_PREV_READS_LEADER);
-        cnt.add_if(run && has, RAFT_C_ENTRY_READS_LEADER);
-        cnt.add_if(run && !okb, RAFT_C_APPEND_SKIPPED);
+        const uint64_t pge = lm(prev >= -1), plt = lm(prev < Llast), p0 = lm(prev >= 0);
+        const uint64_t ok = run & pge & plt;
+        const uint64_t has = pge & lm(i <= Llast);
+        cnt.add(run & p0 & plt, RAFT_C_PREV_READS_LEADER);
+        cnt.add(run & has, RAFT_C_ENTRY_READS_LEADER);
+        cnt.add(run & ~ok, RAFT_C_APPEND_SKIPPED);
+        cnt.add(ok, RAFT_C_APPEND_SENT);
         // every log slot of the tick, resolved up front: the leader's log[prev]
         // and log[i-1], and this replica's own log[prev] (append() :274-276);
         // a handler only writes its own replica's log, so no handler of the
-        // tick can change a slot another one reads.
+        // tick can change a slot another one reads.  The tail caches answer
+        // all but: leader log[prev] below its last two slots, an entry other
+        // than the leader's newest, own log[prev] below the last two slots.
         const uint2* ls = c.lr + (int64_t)(s - c.r) * p.cap;
-        bool h1, h2;
-        int32_t lpt = cached_term(Llast, Lt1, Lt2, prev, h1);
-        int32_t dpt = cached_term(n.last, n.t1, n.t2, prev, h2);
+        int32_t lpt = cached_term(Llast, Lt1, Lt2, prev);
+        int32_t dpt = cached_term(n.last, n.t1, n.t2, prev);
         uint2 lent = make_uint2((uint32_t)Lt1, Lc1);
-        const bool ld1 = ok && prev >= 0 && !h1;
-        const bool ld2 = ok && has && i != Llast;
-        const bool ld3 = ok && prev >= 0 && prev < n.last && !h2;
-        if (__ballot(ld1 || ld2 || ld3)) {                                // rare: tail-cache misses
-            if (ld1) lpt = (int32_t)ls[prev].x;
-            if (ld2) lent = ls[i - 1];
-            if (ld3) dpt = (int32_t)c.lr[prev].x;
+        const uint64_t ld1 = ok & p0 & lm(prev < Llast - 2);
+        const uint64_t ld2 = run & has & lm(i < Llast);
+        const uint64_t ld3 = ok & p0 & lm(prev < n.last - 2);
+        if (ld1 | ld2 | ld3) {                                            // rare: tail-cache misses
+            if (ib(ld1)) lpt = (int32_t)ls[prev].x;
+            if (ib(ld2)) lent = ls[i - 1];
+            if (ib(ld3)) dpt = (int32_t)c.lr[prev].x;
             asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt));   // wait inside the branch
         }
 
-        cnt.add_if(ok, RAFT_C_APPEND_SENT);
-        const bool lreq = ok && lost(p, c, s, c.r, dw, 0);                // :170-172
-        const bool act = ok && !lreq;
+        const uint64_t lreq = ok & lost(p, c, s, c.r, dw, 0);            // :170-172
+        const uint64_t act = ok & ~lreq;
         int32_t rterm;
-        bool succ;
-        const bool answered = append_handler(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
-                                             Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ);
-        const bool lresp = act && answered && lost(p, c, s, c.r, dw, 1);
-        const bool delivered = act && answered && !lresp;
-        cnt.add_if(lreq || lresp, RAFT_C_MSG_DROPPED);
+        uint64_t succ;
+        // no lane of act throws: ok implies prev >= -1
+        append_handler(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
+                       Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ);
+        const uint64_t lresp = act & lost(p, c, s, c.r, dw, 1);
+        const uint64_t delivered = act & ~lresp;
+        cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
         // responses in destination order (S-4).  :146-154 (Q7): a response
         // with a term above the running term adopts it and skips the rest of
         // that response; the running term is the prefix max.
         int32_t T = Lterm;
-        bool sdb = false;                                                 // this response stepped down
-        const uint64_t hib = __ballot(delivered && rterm > Lterm);
+        uint64_t sdb = 0;                                                 // responses that stepped down
+        const uint64_t hib = delivered & lm(rterm > Lterm);
         const bool stepdown = c.gbits(hib) != 0;
         if (hib) {                                                        // wave-uniform, rare
-            const uint32_t dl = c.gbits(__ballot(delivered));
+            const uint32_t dl = c.gbits(delivered);
+            bool sd = false;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 const int32_t rq = bcast(rterm, c.src(q));
-                if (((dl >> q) & 1u) && rq > T) { T = rq; if (c.r == q) sdb = true; }
+                if (((dl >> q) & 1u) && rq > T) { T = rq; if (c.r == q) sd = true; }
             }
+            sdb = lm(sd);
         }
         const int32_t mc_old = n.mc;
-        const bool nd = delivered && !sdb;
-        const bool chk = nd && succ && has;                               // :156-162 (Q9)
-        const bool hbk = nd && succ && !has;                              // :163-164
-        const bool nak = nd && !succ;                                     // :166-167
-        n.nx += chk ? 1 : (nak ? -1 : 0);
-        n.mc = chk ? mc_old + 1 : (hbk ? prev + 1 : mc_old);
-        cnt.add_if(chk, RAFT_C_ENTRIES_ACKED);
+        const uint64_t nd = delivered & ~sdb;
+        const uint64_t chk = nd & succ & has;                             // :156-162 (Q9)
+        const uint64_t hbk = nd & succ & ~has;                            // :163-164
+        const uint64_t nak = nd & ~succ;                                  // :166-167
+        const bool bchk = ib(chk);
+        n.nx += bchk ? 1 : (ib(nak) ? -1 : 0);
+        n.mc = bchk ? mc_old + 1 : (ib(hbk) ? prev + 1 : mc_old);
+        cnt.add(chk, RAFT_C_ENTRIES_ACKED);
         // commit rule, after each acknowledged entry in destination order:
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;
-        const uint64_t ckb = __ballot(chk);
-        if (ckb) {                                                        // wave-uniform
-            const uint32_t ck = c.gbits(ckb);
+        if (chk) {                                                        // wave-uniform
+            const uint32_t ck = c.gbits(chk);
 #pragma unroll
             for (int q = 0; q < R; ++q) {
-                if (!(ckb & L::lanes_of(q))) continue;                    // wave-uniform
+                if (!(chk & L::lanes_of(q))) continue;                    // wave-uniform
                 const int32_t cur = c.r <= q ? n.mc : mc_old;             // rows after / before response q
-                const uint32_t gt = c.gbits(__ballot(cur > C));           // :161
-                const bool inc = ((ck >> q) & 1u) && __popc(gt) >= MAJ;  // :162
-                C += inc ? 1 : 0;
-                cnt.add_if(inc && c.r == q, RAFT_C_COMMITS);
+                const uint32_t gt = c.gbits(lm(cur > C));                 // :161
+                const uint64_t inc = lm((ck >> q) & 1u) & lm(__popc(gt) >= MAJ);   // :162 (whole groups)
+                C += ib(inc) ? 1 : 0;
+                cnt.add(inc & L::lanes_of(q), RAFT_C_COMMITS);
             }
         }
-        const bool wb = run && me;
+        const bool wb = ib(run & mme);
         const bool sd = wb && stepdown;                                   // :148 + offer(FOLLOWER) :152 (S-6)
         n.term = wb ? T : n.term;
         n.commit = wb ? C : n.commit;
@@ -616,21 +632,22 @@ struct Stepper {
         const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
-        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, vr, s, c.dwv, c.s_vote);
-        const bool mine = vr && ((ms >> r) & 1u);
-        const bool lreq = mine && lost(p, c, s, r, dw, 0);          // retry{} swallows, Commons.kt:41
-        const bool act = mine && !lreq;
+        const uint64_t mvr = lm(vr);
+        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
+        const uint64_t mine = mvr & lm((ms >> r) & 1u);
+        const uint64_t lreq = mine & lost(p, c, s, r, dw, 0);       // retry{} swallows, Commons.kt:41
+        const uint64_t act = mine & ~lreq;
         int32_t rterm;
-        bool granted;
+        uint64_t granted;
         vote_handler(n.rep(), act, rt, s + 1, rli, rlt, cnt, rterm, granted);
-        const bool lresp = act && lost(p, c, s, r, dw, 1);
-        const bool delivered = act && !lresp;
-        cnt.add_if(lreq || lresp, RAFT_C_MSG_DROPPED);
+        const uint64_t lresp = act & lost(p, c, s, r, dw, 1);
+        const uint64_t delivered = act & ~lresp;
+        cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
         // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
-        const uint32_t dl = c.gbits(__ballot(delivered));
-        const uint32_t gr = c.gbits(__ballot(delivered && granted));
-        const uint32_t hi = c.gbits(__ballot(delivered && rterm > st));
-        const bool me = vr && r == s;
+        const uint32_t dl = c.gbits(delivered);
+        const uint32_t gr = c.gbits(delivered & granted);
+        const uint32_t hi = c.gbits(delivered & lm(rterm > st));
+        const bool me = ib(mvr & lm(r == s));
         uint32_t f = n.fl & ~(dl << PEND_SH);
         f += (uint32_t)__popc(dl) << LATCH_SH;                      // :209 countDown()
         f += (uint32_t)__popc(gr) << VOTES_SH;                      // :211
@@ -651,52 +668,50 @@ struct Stepper {
         // ---------------- T: timers and election clocks ----------------
         uint32_t send;
         int32_t qt, qli, qlt;
-        bool sstart;
+        uint64_t sstart;
         // a wave where no timer fires and no replica is electing only counts
         // its armed timers down (most waves in steady state)
-        const bool t_armed = n.fl & FL_ARMED;
+        const uint64_t t_armed = lm(n.fl & FL_ARMED);
         const int32_t t_el = n.elec - p.P;
-        if (!__ballot((n.fl & FL_ELECTING) || (t_armed && t_el <= 0))) {
-            n.elec = t_armed ? t_el : n.elec;
-            send = 0u; sstart = false; qt = qli = qlt = 0;
-        } else
-        {
+        const uint64_t t_fire = t_armed & lm(t_el <= 0);                    // Commons.kt:25-27
+        if (!(t_fire | lm(n.fl & FL_ELECTING))) {
+            n.elec = ib(t_armed) ? t_el : n.elec;
+            send = 0u; sstart = 0; qt = qli = qlt = 0;
+        } else {
             uint32_t f = n.fl;
-            const bool armed = f & FL_ARMED;
-            const int32_t el = n.elec - p.P;
-            const bool fire = armed && el <= 0;                             // Commons.kt:25-27
-            n.elec = armed ? (fire ? 0 : el) : n.elec;
+            const bool fire = ib(t_fire);
+            n.elec = ib(t_armed) ? (fire ? 0 : t_el) : n.elec;
             f &= fire ? ~FL_ARMED : ~0u;
             n.role = fire ? (int32_t)RAFT_CANDIDATE : n.role;               // RaftServer.kt:182
-            cnt.add_if(fire, RAFT_C_TIMEOUTS);
-            const bool electing = f & FL_ELECTING;
-            const bool start_fire = fire && !electing;                      // offer(CANDIDATE) :184 -> :65
-            const bool in_round = electing && !(f & FL_BACKOFF);
-            const bool in_bo = electing && (f & FL_BACKOFF);
-            const int32_t ph = n.phase + (in_round ? p.P : (in_bo ? -p.P : 0));   // latch clock :214 / delay :221
+            cnt.add(t_fire, RAFT_C_TIMEOUTS);
+            const uint64_t electing = lm(f & FL_ELECTING), backoff = lm(f & FL_BACKOFF);
+            const uint64_t start_fire = t_fire & ~electing;                 // offer(CANDIDATE) :184 -> :65
+            const uint64_t in_round = electing & ~backoff, in_bo = electing & backoff;
+            const int32_t ph = n.phase + (ib(in_round) ? p.P : (ib(in_bo) ? -p.P : 0));   // latch clock :214 / delay :221
             const uint32_t pend = (f >> PEND_SH) & 0xFFu;
-            const bool rtick = in_round && pend && ph < p.round_to;
-            const int32_t rty = n.retry - (rtick ? p.P : 0);               // retry delay, Commons.kt:43
-            const bool resend = rtick && rty <= 0;
-            const bool bo_end = in_bo && ph <= 0;
-            const bool restart = bo_end && n.role == RAFT_CANDIDATE;        // while (state == CANDIDATE) :191
-            const bool endel = bo_end && !restart;
-            const bool sr = start_fire || restart;                          // round head :191-199
-            n.term += sr ? 1 : 0;                                           // :192
-            n.voted = sr ? r + 1 : n.voted;                                 // :193
+            const uint64_t rtick = in_round & lm(pend != 0) & lm(ph < p.round_to);
+            const int32_t rty = n.retry - (ib(rtick) ? p.P : 0);           // retry delay, Commons.kt:43
+            const uint64_t resend = rtick & lm(rty <= 0);
+            const uint64_t bo_end = in_bo & lm(ph <= 0);
+            const uint64_t restart = bo_end & lm(n.role == RAFT_CANDIDATE); // while (state == CANDIDATE) :191
+            const uint64_t endel = bo_end & ~restart;
+            const uint64_t sr = start_fire | restart;                       // round head :191-199
+            const bool bsr = ib(sr), bend = ib(endel);
+            n.term += bsr ? 1 : 0;                                          // :192
+            n.voted = bsr ? r + 1 : n.voted;                                // :193
             const uint32_t fr = (f & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
-                                (ALL << PEND_SH) | (start_fire ? FL_ELECTING : 0u);
-            n.fl = sr ? fr : (endel ? end_flags(f, n.role) : f);
-            n.phase = (sr || endel) ? 0 : ph;
-            n.retry = (sr || endel) ? 0 : rty;
-            sstart = endel && n.role == RAFT_LEADER;
-            send = sr ? ALL : (resend ? pend : 0u);
+                                (ALL << PEND_SH) | (ib(start_fire) ? FL_ELECTING : 0u);
+            n.fl = bsr ? fr : (bend ? end_flags(f, n.role) : f);
+            n.phase = (bsr || bend) ? 0 : ph;
+            n.retry = (bsr || bend) ? 0 : rty;
+            sstart = endel & lm(n.role == RAFT_LEADER);
+            send = bsr ? ALL : (ib(resend) ? pend : 0u);
             // the RequestVote snapshot, built inside retry{} (:200-207)
             qt = n.term;
             qli = n.last;
             qlt = n.last != 0 ? n.t1 : 0;
-            cnt.add_if((sr || resend) && n.last != 0, RAFT_C_VOTE_LOG_READS);
-            cnt.add_if(sr, RAFT_C_ROUNDS);
+            cnt.add((sr | resend) & lm(n.last != 0), RAFT_C_VOTE_LOG_READS);
+            cnt.add(sr, RAFT_C_ROUNDS);
         }
         start_sessions(p, c, n, sstart, cnt);
         c.clk.mark(PH_T);
@@ -742,7 +757,7 @@ struct Stepper {
 #ifdef RAFT_EXP_EXTRA_PHILOX
         {   // timing experiment only: one more Philox pass of the wave
             const u32x4 x = draw(p, c.t ^ 0x5A5A5A5Au, c.gid(), 77u, (uint32_t)r);
-            cnt.add_if(x.x == 0x12345678u && x.y == 0x9ABCDEF0u && x.z == 1u, RAFT_C_LEADERS);
+            cnt.add(lm(x.x == 0x12345678u), RAFT_C_LEADERS);
         }
 #endif
         c.clk.mark(PH_JOBS);
@@ -777,27 +792,28 @@ struct Stepper {
 
         c.clk.mark(PH_V);
         // ---------------- D: latch closes -> decision (RaftServer.kt:214-222) ----------------
-        bool dstart, need_bo;
+        uint64_t dstart, need_bo;
         {
             const uint32_t f = n.fl;
             const int latch = (f >> LATCH_SH) & 0xF, votes = (f >> VOTES_SH) & 0xF;
-            const bool dec = (f & FL_ELECTING) && !(f & FL_BACKOFF) && (latch >= MAJ || n.phase >= p.round_to);
-            const bool cand = n.role == RAFT_CANDIDATE;
-            const bool win = dec && cand && votes >= MAJ;                   // :218-219
-            need_bo = dec && cand && votes < MAJ;                           // :220-221
-            const bool endel = dec && !need_bo;
+            const uint64_t dec = lm(f & FL_ELECTING) & ~lm(f & FL_BACKOFF) &
+                                 (lm(latch >= MAJ) | lm(n.phase >= p.round_to));
+            const uint64_t cand = dec & lm(n.role == RAFT_CANDIDATE);
+            const uint64_t win = cand & lm(votes >= MAJ);                   // :218-219
+            need_bo = cand & ~win;                                          // :220-221
+            const uint64_t endel = dec & ~need_bo;
             const uint32_t fc = f & ~(0xFFu << PEND_SH);                    // cancelChildren() :215
-            n.role = win ? (int32_t)RAFT_LEADER : n.role;
+            n.role = ib(win) ? (int32_t)RAFT_LEADER : n.role;
             const uint32_t fb = (fc & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
-            n.fl = endel ? end_flags(fc, n.role) : (need_bo ? fb : f);
-            n.phase = endel ? 0 : n.phase;
-            n.retry = dec ? 0 : n.retry;
-            dstart = endel && n.role == RAFT_LEADER;
+            n.fl = ib(endel) ? end_flags(fc, n.role) : (ib(need_bo) ? fb : f);
+            n.phase = ib(endel) ? 0 : n.phase;
+            n.retry = ib(dec) ? 0 : n.retry;
+            dstart = endel & lm(n.role == RAFT_LEADER);
         }
-        if (__ballot(need_bo)) {
+        if (need_bo) {
             const uint32_t w = timer_word(p, c);
             const KernArgs kp = kernargs();
-            if (need_bo) n.phase = scale_range(w, kp->bmin, kp->bmax);
+            if (ib(need_bo)) n.phase = scale_range(w, kp->bmin, kp->bmax);
         }
         start_sessions(p, c, n, dstart, cnt);
         c.clk.mark(PH_D);
@@ -827,30 +843,31 @@ struct Stepper {
         const uint64_t cmd_thr = kp->cmd_thr32;
         if (cmd_thr) {
             const int32_t cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
-            const uint32_t lead = c.gbits(__ballot(n.role == RAFT_LEADER));
-            const bool cm = (cmd_limit == 0 || n.cmdc < cmd_limit) && hw1 < cmd_thr && lead;
-            const bool tgt = cm && (cmd_mode == RAFT_CMD_LOWEST_LEADER ? r == __builtin_ctz(lead)
-                                                                       : ((lead >> r) & 1u) != 0);
+            const uint64_t isl = lm(n.role == RAFT_LEADER);
+            const uint32_t lead = c.gbits(isl);
+            const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
+                                lm(lead != 0);
+            const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
             append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
-            n.cmdc += cm ? 1 : 0;
+            n.cmdc += ib(cm) ? 1 : 0;
         }
 
         c.clk.mark(PH_C);
         // ---------------- K: end-of-step observations ----------------
         {
-            const bool isl = n.role == RAFT_LEADER;
-            const uint32_t lead = c.gbits(__ballot(isl));
-            cnt.add_if(isl, RAFT_C_LEADERS);
-            cnt.add_if(lead && r == __builtin_ctz(lead), RAFT_C_GROUPS_WITH_LEADER);
-            if (__ballot(__popc(lead) >= 2)) {                              // rare
+            const uint64_t isl = lm(n.role == RAFT_LEADER);
+            const uint32_t lead = c.gbits(isl);
+            cnt.add(isl, RAFT_C_LEADERS);
+            cnt.add(lm(lead != 0) & L::lanes_of(0), RAFT_C_GROUPS_WITH_LEADER);   // one lane per group
+            if (lm(__popc(lead) >= 2)) {                                    // rare
                 bool dual = false;
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
                     const int32_t tq = bcast(n.term, c.src(q));
-                    if (isl && r < q && ((lead >> q) & 1u) && tq == n.term) dual = true;
+                    if (ib(isl) && r < q && ((lead >> q) & 1u) && tq == n.term) dual = true;
                 }
-                const uint32_t db = c.gbits(__ballot(dual));
-                cnt.add_if(db && r == 0, RAFT_C_DUAL_LEADER_GROUPS);
+                const uint32_t db = c.gbits(lm(dual));
+                cnt.add(lm(db != 0) & L::lanes_of(0), RAFT_C_DUAL_LEADER_GROUPS);
             }
         }
 
