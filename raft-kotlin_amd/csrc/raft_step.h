@@ -558,14 +558,17 @@ struct Stepper {
             asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt));   // wait inside the branch
         }
 
+        // both directions' losses resolved here: a lane mask of comparisons made
+        // in an earlier basic block (before the handler's log store) would be
+        // re-materialised through a VGPR
         const uint64_t lreq = ok & lost(p, c, s, c.r, dw, 0);            // :170-172
         const uint64_t act = ok & ~lreq;
+        const uint64_t lresp = act & lost(p, c, s, c.r, dw, 1);
         int32_t rterm;
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
         append_handler(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
                        Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ);
-        const uint64_t lresp = act & lost(p, c, s, c.r, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
