@@ -237,6 +237,22 @@ def main():
                   "frac": s_ach / HBM_PEAK_GBS, "traffic": s_tr["bytes_per_launch"] if s_tr else None,
                   "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
+    # ---- safety flags (untimed): the run's counter-borne flags plus the
+    # Log Matching check over committed prefixes ----
+    mism = eng.check_log_matching()
+    if world > 1:
+        t = torch.tensor([mism], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        mism = int(t.item())
+    safety = {
+        "log_matching_mismatched_groups": mism,
+        "commit_regressions": int(c_all[:, abi.C_INDEX["commit_regressions"]].sum()),
+        "dual_leader_group_steps": int(c_all[:, abi.C_INDEX["dual_leader_groups"]].sum()),
+        "log_overflow": overflow,
+        "note": "observations of the reference's protocol (quirks Q4/Q9 do not preserve these "
+                "properties); over the timed steps, Log Matching at the end of the run",
+    }
+
     out = {
         "metric": METRIC,
         "value": value,
@@ -270,6 +286,7 @@ def main():
         },
         "roofline_streaming": stream,
         "valid": overflow == 0,
+        "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -220,6 +220,16 @@ int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* 
  * physLen included): sum over groups of a per-group hash. */
 int raft_engine_digest(raft_engine* e, uint64_t* out);
 
+/* Log Matching over committed prefixes (safety flag): a
+ * group of [g0, g0+n) is flagged when two of its replicas hold different
+ * (term, cmd) at an index inside both replicas' committed prefixes, i.e.
+ * i < min(commitIndex, lastIndex) of each.  The reference's quirks (Q4 commit
+ * clamp, Q9 no current-term guard) do not preserve this property, so the
+ * count is an observation about the reference's protocol, not an engine
+ * error.  *mismatched = flagged groups; flags (nullable, host, n bytes)
+ * receives 1 per flagged group. */
+int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_t* flags, int64_t* mismatched);
+
 /* ---- single-handler batches: the service boundary ----------------------
  * group: engine-local group index; dst: replica index 0..R-1.  Messages
  * to the same (group, dst) are applied in batch order.  Effects on the

@@ -178,6 +178,7 @@ def load_library(path: str | None = None):
         "raft_engine_read_log": (C.c_int, [eng, I64, I64, P(I32), P(C.c_uint32)]),
         "raft_engine_write_log": (C.c_int, [eng, I64, I64, P(I32), P(C.c_uint32)]),
         "raft_engine_digest": (C.c_int, [eng, P(U64)]),
+        "raft_engine_check_log_matching": (C.c_int, [eng, I64, I64, P(C.c_uint8), P(I64)]),
         "raft_vote_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_vote_req), P(raft_vote_resp), I64]),
         "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
         "raft_append_command_batch": (C.c_int, [eng, P(I64), P(I32), P(C.c_uint32), I64]),
@@ -199,6 +200,6 @@ EXPORTED_SYMBOLS = [
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
-    "raft_engine_write_log", "raft_engine_digest", "raft_vote_batch", "raft_append_batch",
+    "raft_engine_write_log", "raft_engine_digest", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_philox4x32_10",
 ]

@@ -329,6 +329,45 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 
 // order-independent state digest: sum of per-group FNV-1a/fmix64
 template <int R>
+__global__ __launch_bounds__(BLOCK) void log_match_kernel(DevParams p, int64_t g0, int64_t n, uint8_t* flags,
+                                                         unsigned long long* count) {
+    // one wave per group; the lanes stride the log indices, so each replica's
+    // committed prefix is read as coalesced 512-B runs
+    const int lane = threadIdx.x & 63;
+    const int64_t k = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (k >= n) return;                                                   // wave-uniform
+    const int64_t g = g0 + k;
+    int32_t c[R];
+    int32_t cmax = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t idx = g * R + r;
+        const int32_t cm = min(p.st[fidx(p, RAFT_F_COMMIT, idx)], p.st[fidx(p, RAFT_F_LAST, idx)]);
+        c[r] = max(0, min(cm, p.cap));
+        cmax = max(cmax, c[r]);
+    }
+    bool bad = false;
+    for (int32_t i = lane; i < cmax; i += 64) {
+        bool have = false;
+        uint2 ref = make_uint2(0u, 0u);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (i < c[r]) {
+                const uint2 v = p.log[(g * R + r) * (int64_t)p.cap + i];
+                bad |= have && (v.x != ref.x || v.y != ref.y);
+                ref = have ? ref : v;
+                have = true;
+            }
+        }
+    }
+    const bool any = __ballot(bad) != 0;
+    if (lane == 0) {
+        if (flags) flags[k] = any ? 1 : 0;
+        if (any) atomicAdd(count, 1ull);
+    }
+}
+
+template <int R>
 __global__ __launch_bounds__(BLOCK) void digest_kernel(DevParams p, unsigned long long* out) {
     __shared__ unsigned long long part[WAVES_PER_BLOCK];
     const int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -518,6 +557,12 @@ template <int R> struct PackL {
 template <int R> struct UnpackL {
     static void run(raft_engine* e, int64_t g0, int64_t n, const int32_t* buf) {
         unpack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, g0, n, buf);
+    }
+};
+template <int R> struct LogMatchL {
+    static void run(raft_engine* e, int64_t g0, int64_t n, uint8_t* flags, unsigned long long* count) {
+        const unsigned grid = (unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+        log_match_kernel<R><<<grid, BLOCK, 0, e->stream>>>(e->dp, g0, n, flags, count);
     }
 };
 template <int R> struct DigestL {
@@ -848,6 +893,31 @@ int raft_engine_digest(raft_engine* e, uint64_t* out) {
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     (void)hipFree(d);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
+int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_t* flags, int64_t* mismatched) {
+    if (int rc = check_range(e, g0, n)) return rc;
+    if (!mismatched) return fail(RAFT_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(e->device));
+    *mismatched = 0;
+    if (n == 0) return RAFT_OK;
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, 8 + (flags ? (size_t)n : 0)));
+    unsigned long long* cnt = (unsigned long long*)d;
+    uint8_t* fl = flags ? (uint8_t*)d + 8 : nullptr;
+    unsigned long long h = 0;
+    hipError_t err = hipMemsetAsync(d, 0, 8, e->stream);
+    if (err == hipSuccess) {
+        dispatch_R<LogMatchL>(e->p.R, e, g0, n, fl, cnt);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) err = hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess && flags) err = hipMemcpyAsync(flags, fl, (size_t)n, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    *mismatched = (int64_t)h;
     return RAFT_OK;
 }
 

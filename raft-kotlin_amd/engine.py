@@ -139,6 +139,17 @@ class RaftEngine:
         self._check(self._lib.raft_engine_digest(self._h, C.byref(out)), "digest")
         return int(out.value)
 
+    def check_log_matching(self, g0: int = 0, n: int | None = None, flags: bool = False):
+        """Groups whose replicas disagree inside their common committed prefix
+        (safety flag, include/raft_engine.h); returns the count, or (count,
+        per-group uint8 flags) with flags=True."""
+        n = self.G - g0 if n is None else n
+        f = np.zeros(n, dtype=np.uint8) if flags else None
+        out = C.c_int64()
+        self._check(self._lib.raft_engine_check_log_matching(self._h, g0, n, abi.ptr(f, C.c_uint8) if flags else None,
+                                                             C.byref(out)), "check_log_matching")
+        return (int(out.value), f) if flags else int(out.value)
+
     # -- the service boundary (RaftServer.kt:228-287, :100-107) -------------
     def vote_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
         """req: [n, 4] int32 (term, candidateId, lastLogIndex, lastLogTerm) ->

@@ -13,8 +13,8 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import (abi, assert_same_logs, assert_same_state, blank_groups, fld, set_fld, set_session,
-                     session)
+from helpers import (abi, assert_same_logs, assert_same_state, blank_groups, fld, log_matching_flags, set_fld,
+                     set_session, session)
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +53,46 @@ def run_lockstep(e, o, steps, chunk, label, digest_every=1):
     return se, ov
 
 
+def check_log_matching(e, o, label):
+    """The kernel's Log Matching flags vs the numpy restatement on the oracle's logs."""
+    so = o.read_state()
+    t, c = o.read_log()
+    want = log_matching_flags(so, t, c, e.R)
+    n, got = e.check_log_matching(flags=True)
+    assert np.array_equal(got, want), f"{label}: log-matching flags differ in {np.count_nonzero(got != want)} groups"
+    assert n == int(want.sum())
+    return n
+
+
+def test_log_matching_check_crafted():
+    """Flags exactly the groups whose replicas differ inside both committed prefixes."""
+    R, G, cap = 3, 6, 16
+    e = RaftEngine(abi.make_params(R=R, G=G, log_cap=cap))
+    w = blank_groups(G, R)
+    t = np.zeros((G, R, cap), np.int32)
+    c = np.zeros((G, R, cap), np.uint32)
+    for g in range(G):
+        for r in range(R):
+            set_fld(w, R, r, "last", 8)
+            set_fld(w, R, r, "phys", 8)
+            set_fld(w, R, r, "commit", 6)
+            t[g, r, :8] = np.arange(1, 9)
+            c[g, r, :8] = 100 + np.arange(8)
+    c[1, 2, 5] += 1                      # inside every committed prefix -> flagged
+    t[2, 1, 6] = 99                      # beyond the committed prefixes -> not flagged
+    set_fld(w[3:4], R, 0, "commit", 3)   # replica 0's prefix is short ...
+    t[3, 0, 3] = 99                      # ... so index 3 of it is not covered -> not flagged
+    set_fld(w[4:5], R, 1, "last", 5)     # commit 6 > lastIndex 5 clamps to 5 ...
+    t[4, 1, 5] = 77                      # ... so index 5 is not covered -> not flagged
+    t[5, 0, 0] = 42                      # index 0 -> flagged
+    e.write_state(w)
+    e.write_log(t, c)
+    n, f = e.check_log_matching(flags=True)
+    want = log_matching_flags(w, t, c, R)
+    assert list(f) == list(want)
+    assert n == 2 and list(np.nonzero(f)[0]) == [1, 5]
+
+
 def test_init_state_matches_oracle():
     e, o = pair(R=5, G=1000, seed=9, log_cap=16)
     assert_same_state(e.read_state(), o.read_state(), 5, "init")
@@ -89,6 +129,7 @@ def test_config3_drops_churn_reduced():
     e, o = pair(log_cap=768, **kw)
     se, ov = run_lockstep(e, o, 2_000, 100, "config3", digest_every=5)
     assert ov == 0
+    check_log_matching(e, o, "config3")
 
 
 def test_config5_partitions_reduced():
@@ -97,6 +138,7 @@ def test_config5_partitions_reduced():
     kw.update(G=2_000)
     e, o = pair(log_cap=2600, **kw)
     run_lockstep(e, o, 1_500, 100, "config5", digest_every=3)
+    check_log_matching(e, o, "config5")
 
 
 @pytest.mark.parametrize("R", [1, 2, 3, 4, 6, 8])
