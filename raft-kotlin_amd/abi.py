@@ -183,6 +183,17 @@ def load_library(path: str | None = None):
         "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
         "raft_append_command_batch": (C.c_int, [eng, P(I64), P(I32), P(C.c_uint32), I64]),
         "raft_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+        # include/raft_wire.h
+        "raft_wire_decode_vote_req": (C.c_int, [P(C.c_uint8), P(I64), I64, P(raft_vote_req)]),
+        "raft_wire_encode_vote_req": (I64, [P(raft_vote_req), I64, P(C.c_uint8), I64, P(I64)]),
+        "raft_wire_decode_vote_resp": (C.c_int, [P(C.c_uint8), P(I64), I64, P(raft_vote_resp)]),
+        "raft_wire_encode_vote_resp": (I64, [P(raft_vote_resp), I64, P(C.c_uint8), I64, P(I64)]),
+        "raft_wire_decode_append_req": (C.c_int, [P(C.c_uint8), P(I64), I64, P(raft_append_req), P(I64), P(I32),
+                                                  P(I32)]),
+        "raft_wire_encode_append_req": (I64, [P(raft_append_req), P(C.c_uint8), P(I64), I64, P(C.c_uint8), I64,
+                                              P(I64)]),
+        "raft_wire_decode_append_resp": (C.c_int, [P(C.c_uint8), P(I64), I64, P(raft_append_resp)]),
+        "raft_wire_encode_append_resp": (I64, [P(raft_append_resp), I64, P(C.c_uint8), I64, P(I64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -192,7 +203,7 @@ def load_library(path: str | None = None):
     return lib
 
 
-# symbols declared in include/raft_engine.h (checked by tests/test_abi.py)
+# symbols declared in include/*.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "raft_params_default", "raft_last_error", "raft_abi_version", "raft_engine_create",
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
@@ -202,4 +213,8 @@ EXPORTED_SYMBOLS = [
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_philox4x32_10",
+    # include/raft_wire.h
+    "raft_wire_decode_vote_req", "raft_wire_encode_vote_req", "raft_wire_decode_vote_resp",
+    "raft_wire_encode_vote_resp", "raft_wire_decode_append_req", "raft_wire_encode_append_req",
+    "raft_wire_decode_append_resp", "raft_wire_encode_append_resp",
 ]

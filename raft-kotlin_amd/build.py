@@ -11,8 +11,9 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "raft_engine.hip")
+SRCS = [SRC, os.path.join(PKG, "csrc", "raft_wire.cpp")]          # the wire codec is host code
 HDRS = [os.path.join(PKG, "csrc", h) for h in ("raft_step.h", "philox.h")] + [
-    os.path.join(ROOT, "include", "raft_engine.h")]
+    os.path.join(ROOT, "include", h) for h in ("raft_engine.h", "raft_wire.h")]
 OUT = os.path.join(PKG, "lib", "libraft_engine.so")
 ARCH = os.environ.get("RAFT_OFFLOAD_ARCH", "gfx950")
 
@@ -28,7 +29,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(f) > t for f in [SRC, *HDRS, __file__])
+    return any(os.path.getmtime(f) > t for f in [*SRCS, *HDRS, __file__])
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -37,7 +38,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC]
+           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -571,6 +571,9 @@ template <int R> struct DigestL {
     }
 };
 
+// raft_wire.cpp reports its errors through raft_last_error() too
+int raft_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+
 static uint64_t ppm_thr(uint32_t ppm, int bits) {
     // smallest u with u * 1e6 >= ppm << bits  ==  ceil(ppm * 2^bits / 1e6)
     const unsigned __int128 num = (unsigned __int128)ppm << bits;

@@ -21,11 +21,11 @@ engine stores a u32 id per entry, interned here.  Every call is one HIP batch;
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 
-from . import abi
+from . import abi, wire
 from .engine import RaftEngine
 
 
@@ -173,3 +173,24 @@ class RaftService:
                 raise IndexError("Log.get: prevLogIndex out of bounds (RaftServer.kt:276, Commons.kt:53-54)")
             res.append(ResponseAppendEntriesRPC(int(t), bool(s)))
         return res
+
+    # -- the gRPC-facing wire form (include/raft_wire.h) --------------------
+    # RaftImplBase.vote()/append() (RaftServer.kt:228, :253) receive and return
+    # serialized protobufs; these batch them through the engine unchanged.
+    def vote_wire(self, groups, replicas, requests: List[bytes]) -> List[bytes]:
+        """Serialized RequestVoteRPCs -> serialized ResponseVoteRPCs."""
+        q = wire.decode_vote_requests(requests)
+        return wire.encode_vote_responses(self.engine.vote_batch(groups, replicas, q))
+
+    def append_wire(self, groups, replicas, requests: List[bytes]) -> List[Optional[bytes]]:
+        """Serialized RequestAppendEntriesRPCs -> serialized responses; None where
+        the handler threw (Log.get, RaftServer.kt:276): that call has no response,
+        which the reference's caller swallows (RaftServer.kt:170-172)."""
+        rows, cmds, _ = wire.decode_append_requests(requests)
+        rows = rows.astype(np.int64)
+        for m, c in enumerate(cmds):
+            if c is not None:
+                rows[m, 6] = self.commands.intern(c.decode("utf-8"))
+        out = self.engine.append_batch(groups, replicas, rows)
+        enc = wire.encode_append_responses(out)
+        return [None if out[m, 2] else enc[m] for m in range(len(enc))]

@@ -1,4 +1,4 @@
-"""The C-ABI library: loads, exports every symbol include/raft_engine.h declares,
+"""The C-ABI library: loads, exports every symbol include/*.h declares,
 reports a clean error without a GPU, and its host-side Philox matches the KATs.
 No compute runs here (CPU-only container)."""
 import ctypes as C
@@ -13,11 +13,12 @@ import pytest
 from helpers import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "raft_engine.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = re.findall(r"\b(raft_[a-z0-9_]+)\s*\(", src)
     return sorted(set(n for n in names if n != "raft_group_words"))   # static inline helper

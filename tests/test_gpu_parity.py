@@ -258,6 +258,44 @@ def test_handler_batches_vs_oracle():
     assert_same_logs(se, e.read_log(), o.read_log(), R, "handlers")
 
 
+def test_service_wire_path_matches_batches():
+    """RaftService.vote_wire / append_wire (serialized protobufs through
+    include/raft_wire.h) leave the same responses and state as the fixed-width
+    batch entry points on an identical engine."""
+    service_mod = importlib.import_module("raft-kotlin_amd.service")
+    wire = importlib.import_module("raft-kotlin_amd.wire")
+    rng = np.random.default_rng(11)
+    R, G, cap, n = 5, 32, 8, 800
+    w, lt, lc = random_states(rng, G, R, cap)
+    a, b = (RaftEngine(abi.make_params(R=R, G=G, log_cap=cap, seed=3)) for _ in range(2))
+    for x in (a, b):
+        x.write_state(w)
+        x.write_log(lt, lc)
+    svc = service_mod.RaftService(b)
+    grp = rng.integers(0, G, size=n)
+    dst = rng.integers(0, R, size=n).astype(np.int32)
+    vq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(0, cap + 1, n),
+                   rng.integers(0, 4, n)], axis=1).astype(np.int32)
+    got = wire.decode_vote_responses(svc.vote_wire(grp, dst, wire.encode_vote_requests(vq)))
+    assert np.array_equal(got, a.vote_batch(grp, dst, vq))
+    names = [f"cmd-{i}".encode() for i in range(7)]
+    aq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(-2, cap, n),
+                   rng.integers(-1, 4, n), rng.integers(0, 2, n), rng.integers(0, 6, n),
+                   np.zeros(n), rng.integers(0, 8, n)], axis=1).astype(np.int32)
+    cmds = [names[rng.integers(0, 7)] if q[4] else None for q in aq]
+    resp = svc.append_wire(grp, dst, wire.encode_append_requests(aq, cmds))
+    aq64 = aq.astype(np.int64)
+    aq64[:, 6] = [svc.commands.intern(c.decode()) if c is not None else 0 for c in cmds]
+    ref = a.append_batch(grp, dst, aq64)
+    for m, r in enumerate(resp):
+        if ref[m, 2]:
+            assert r is None                                   # the handler threw: no response
+        else:
+            assert np.array_equal(wire.decode_append_responses([r])[0, :2], ref[m, :2])
+    assert np.array_equal(a.read_state(), b.read_state())
+    assert a.digest() == b.digest()
+
+
 def test_kats_on_engine():
     """K2-K4 and K6/K7 traces replayed through the engine's C-ABI."""
     R = 3

@@ -1,0 +1,160 @@
+"""The proto3 wire codec (include/raft_wire.h) against the protobuf runtime.
+
+The message classes are built at run time from a descriptor of
+greeter.proto:16-44 (field numbers and types as in the reference), so the
+checker is protobuf's own encoder/parser.  Host code only: runs on CPU."""
+import importlib
+
+import numpy as np
+import pytest
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+wire = importlib.import_module("raft-kotlin_amd.wire")
+
+I32, BOOL, STR, MSG = (descriptor_pb2.FieldDescriptorProto.TYPE_INT32, descriptor_pb2.FieldDescriptorProto.TYPE_BOOL,
+                       descriptor_pb2.FieldDescriptorProto.TYPE_STRING, descriptor_pb2.FieldDescriptorProto.TYPE_MESSAGE)
+OPT, REP = descriptor_pb2.FieldDescriptorProto.LABEL_OPTIONAL, descriptor_pb2.FieldDescriptorProto.LABEL_REPEATED
+
+
+def _msg(fd, name, fields, nested=()):
+    m = fd.message_type.add() if not isinstance(fd, descriptor_pb2.DescriptorProto) else fd.nested_type.add()
+    m.name = name
+    for num, fname, typ, *rest in fields:
+        f = m.field.add()
+        f.name, f.number, f.type = fname, num, typ
+        f.label = rest[1] if len(rest) > 1 else OPT
+        if typ == MSG:
+            f.type_name = rest[0]
+    for n in nested:
+        _msg(m, *n)
+    return m
+
+
+@pytest.fixture(scope="module")
+def pb():
+    fd = descriptor_pb2.FileDescriptorProto(name="greeter_test.proto", package="ua.org.kug.raft", syntax="proto3")
+    _msg(fd, "RequestVoteRPC", [(1, "term", I32), (2, "candidateId", I32), (3, "lastLogIndex", I32),
+                                (4, "lastLogTerm", I32)])
+    _msg(fd, "ResponseVoteRPC", [(1, "term", I32), (2, "voteGranted", BOOL)])
+    _msg(fd, "RequestAppendEntriesRPC",
+         [(1, "term", I32), (2, "leaderId", I32), (3, "prevLogIndex", I32), (4, "prevLogTerm", I32),
+          (5, "entries", MSG, ".ua.org.kug.raft.RequestAppendEntriesRPC.LogEntry", REP), (6, "leaderCommit", I32)],
+         nested=[("LogEntry", [(1, "term", I32), (2, "command", STR)])])
+    _msg(fd, "ResponseAppendEntriesRPC", [(1, "term", I32), (2, "success", BOOL)])
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    get = lambda n: message_factory.GetMessageClass(pool.FindMessageTypeByName("ua.org.kug.raft." + n))
+    return {n: get(n) for n in ("RequestVoteRPC", "ResponseVoteRPC", "RequestAppendEntriesRPC",
+                                "ResponseAppendEntriesRPC")}
+
+
+rng = np.random.default_rng(7)
+
+
+def ints(n):
+    """int32 values with zeros, small, negative and extreme ones."""
+    pool = np.array([0, 1, -1, 127, 128, 16383, 16384, 2**31 - 1, -2**31, 300, -300], dtype=np.int64)
+    v = np.where(rng.random(n) < 0.5, rng.choice(pool, n), rng.integers(-2**31, 2**31, n))
+    return v.astype(np.int32)
+
+
+def test_vote_request_roundtrip(pb):
+    n = 500
+    q = np.stack([ints(n) for _ in range(4)], 1)
+    ref = [pb["RequestVoteRPC"](term=int(a), candidateId=int(b), lastLogIndex=int(c), lastLogTerm=int(d))
+           .SerializeToString() for a, b, c, d in q]
+    assert wire.encode_vote_requests(q) == ref                         # canonical bytes
+    assert np.array_equal(wire.decode_vote_requests(ref), q)
+
+
+def test_responses_roundtrip(pb):
+    n = 300
+    r = np.stack([ints(n), rng.integers(0, 2, n).astype(np.int32)], 1)
+    for name, enc, dec, flag in (("ResponseVoteRPC", wire.encode_vote_responses, wire.decode_vote_responses,
+                                  "voteGranted"),
+                                 ("ResponseAppendEntriesRPC", wire.encode_append_responses,
+                                  wire.decode_append_responses, "success")):
+        ref = [pb[name](term=int(t), **{flag: bool(g)}).SerializeToString() for t, g in r]
+        rows = np.concatenate([r, np.zeros((n, 1), np.int32)], 1) if name.startswith("ResponseAppend") else r
+        assert enc(rows) == ref
+        got = dec(ref)
+        assert np.array_equal(got[:, :2], r)
+        for b, (t, g) in zip(ref, got[:, :2]):
+            m = pb[name]()
+            m.ParseFromString(b)
+            assert (m.term, getattr(m, flag)) == (t, bool(g))
+
+
+def append_case(pb, n=400):
+    cmds = ["", "x", "set k=v", "ключ", "a" * 200, "☃ snow"]
+    rows, commands, msgs = [], [], []
+    for m in range(n):
+        t, lid, pi, pt, lc = (int(x) for x in ints(5))
+        k = int(rng.choice([0, 1, 1, 1, 2, 3]))
+        ents = [(int(ints(1)[0]), str(rng.choice(cmds))) for _ in range(k)]
+        msg = pb["RequestAppendEntriesRPC"](term=t, leaderId=lid, prevLogIndex=pi, prevLogTerm=pt, leaderCommit=lc)
+        for et, ec in ents:
+            msg.entries.add(term=et, command=ec)
+        msgs.append(msg.SerializeToString())
+        rows.append([t, lid, pi, pt, int(k > 0), ents[0][0] if k else 0, 0, lc])
+        commands.append(ents[0][1].encode() if k else None)
+    return np.array(rows, np.int32), commands, msgs
+
+
+def test_append_request_decode(pb):
+    rows, commands, msgs = append_case(pb)
+    got, cmds, ne = wire.decode_append_requests(msgs)
+    assert np.array_equal(got, rows)
+    assert cmds == commands
+    for b, k in zip(msgs, ne):
+        m = pb["RequestAppendEntriesRPC"]()
+        m.ParseFromString(b)
+        assert len(m.entries) == k
+
+
+def test_append_request_encode_single_entry(pb):
+    """Encoding carries entries[0] only (RaftServer.kt:130-132 sends at most one)."""
+    rows, commands, msgs = append_case(pb)
+    one = []
+    for b in msgs:
+        m = pb["RequestAppendEntriesRPC"]()
+        m.ParseFromString(b)
+        del m.entries[1:]
+        one.append(m.SerializeToString())
+    assert wire.encode_append_requests(rows, commands) == one
+
+
+def test_noncanonical_encodings(pb):
+    """Reordered and repeated fields (last wins), unknown fields of every wire
+    type, non-minimal varints: decoded as protobuf parses them."""
+    def key(num, wt):
+        return bytes([num << 3 | wt])
+    unknown = key(9, 0) + b"\x96\x01" + key(10, 5) + b"abcd" + key(11, 1) + b"abcdefgh" + key(12, 2) + b"\x03xyz"
+    b = (unknown + key(4, 0) + b"\x05" + key(1, 0) + b"\x07" + key(1, 0) + b"\x09" + key(3, 0) +
+         b"\x83\x80\x80\x00" + key(2, 2) + b"\x01z" + key(2, 0) + b"\x02")   # field 2 as bytes: unknown type
+    m = pb["RequestVoteRPC"]()
+    m.ParseFromString(b)
+    got = wire.decode_vote_requests([b])[0]
+    assert list(got) == [m.term, m.candidateId, m.lastLogIndex, m.lastLogTerm] == [9, 2, 3, 5]
+    # LogEntry with unknown fields and two entries: entries[0] wins
+    e0 = key(3, 0) + b"\x01" + key(2, 2) + b"\x02hi" + key(1, 0) + b"\x04"
+    e1 = key(1, 0) + b"\x05" + key(2, 2) + b"\x02no"
+    b = key(5, 2) + bytes([len(e0)]) + e0 + key(6, 0) + b"\x08" + key(5, 2) + bytes([len(e1)]) + e1
+    m = pb["RequestAppendEntriesRPC"]()
+    m.ParseFromString(b)
+    rows, cmds, ne = wire.decode_append_requests([b])
+    assert (rows[0, 4], rows[0, 5], rows[0, 7], cmds[0], ne[0]) == (1, m.entries[0].term, m.leaderCommit,
+                                                                     m.entries[0].command.encode(), 2)
+
+
+@pytest.mark.parametrize("bad", [b"\x08", b"\x08\x80", b"\x12\x05ab", b"\x0b", b"\x0f\x00", b"\x00\x01",
+                                 b"\x08" + b"\xff" * 10 + b"\x01"])
+def test_malformed_messages_fail(bad):
+    with pytest.raises(RuntimeError, match="malformed"):
+        wire.decode_vote_requests([b"\x08\x01", bad])
+
+
+def test_empty_batches():
+    assert wire.decode_vote_requests([]).shape == (0, 4)
+    assert wire.encode_vote_responses(np.zeros((0, 2), np.int32)) == []
+    assert wire.encode_vote_requests(np.zeros((1, 4), np.int32)) == [b""]
