@@ -82,21 +82,32 @@ def cpu_baseline(args, kw, log_cap, total_steps):
     probe.step(args.cpu_chunk, nthreads=threads, counters=False)
     rate = args.cpu_groups * args.cpu_chunk / max(1e-6, time.perf_counter() - t0)
     probe.close()
+
+    def timed(G, nthreads):
+        o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
+        o.step(args.warmup, nthreads=nthreads, counters=False)
+        t0 = time.perf_counter()
+        done = 0
+        while done < total_steps - args.warmup:
+            k = min(args.cpu_chunk * 10, total_steps - args.warmup - done)
+            o.step(k, nthreads=nthreads, counters=True)
+            done += k
+        dt = time.perf_counter() - t0
+        o.close()
+        return G * done / dt, dt
+
     G = int(min(kw["G"], max(threads * 64, rate * args.cpu_seconds / total_steps)))
-    o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
-    o.step(args.warmup, nthreads=threads, counters=False)
-    t0 = time.perf_counter()
-    done = 0
-    while done < total_steps - args.warmup:
-        k = min(args.cpu_chunk * 10, total_steps - args.warmup - done)
-        o.step(k, nthreads=threads, counters=True)
-        done += k
-    dt = time.perf_counter() - t0
-    o.close()
-    return {"value": G * done / dt, "unit": "group-steps/s", "cores": threads, "kind": "port",
+    value, dt = timed(G, threads)
+    # the single-thread rate on a smaller sample of the same groups
+    G1 = int(min(kw["G"], max(64, rate / threads * args.cpu_seconds_1t / total_steps)))
+    value1, dt1 = timed(G1, 1)
+    return {"value": value, "unit": "group-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle/raft_oracle.c (scalar C restatement of RaftServer.kt/Commons.kt), global groups "
                       f"0..{G - 1} of the same config for the same {total_steps} steps as the GPU "
-                      f"({args.warmup} untimed), {dt:.1f} s, pthreads over groups"}
+                      f"({args.warmup} untimed), {dt:.1f} s, pthreads over groups",
+            "single_thread": {"value": value1, "unit": "group-steps/s", "cores": 1,
+                              "sample": f"global groups 0..{G1 - 1}, same steps, {dt1:.1f} s"},
+            "host_cpus": os.cpu_count()}
 
 
 def main():
@@ -117,6 +128,7 @@ def main():
     ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds-1t", type=float, default=5.0, help="target seconds of the single-thread CPU leg")
     ap.add_argument("--cpu-chunk", type=int, default=20)
     ap.add_argument("--warmup-cpu", type=int, default=40)
     args = ap.parse_args()
