@@ -110,6 +110,14 @@ __device__ __forceinline__ KernArgs kernargs() {
 // positive mask, so dead lanes (inert nodes) never satisfy a predicate.
 __device__ __forceinline__ uint64_t lm(bool cmp) { return __ballot(cmp); }
 __device__ __forceinline__ bool ib(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+// x + 1 on the lanes of m: one v_addc_co_u32 with the mask as carry-in (the
+// compiler would emit a v_cndmask and a v_add)
+__device__ __forceinline__ int32_t inc_if(int32_t x, uint64_t m) {
+    int32_t y;
+    uint64_t carry;
+    asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(y), "=s"(carry) : "v"(x), "s"(m));
+    return y;
+}
 
 // Step counters of a wave.  add(m, c) adds popcount(m) -- the lanes where
 // counter c's event happened -- into the wave-uniform (SGPR) total of counter
@@ -334,6 +342,12 @@ struct Lanes {
     static constexpr bool VOTE_JOB = JOBS && J_VOTE + NCH <= R;
 
     // lanes whose replica index is s (compile-time masks)
+    // lanes whose replica index is <= s
+    static constexpr uint64_t lanes_upto(int s) {
+        uint64_t m = 0;
+        for (int q = 0; q <= s; ++q) m |= lanes_of(q);
+        return m;
+    }
     static constexpr uint64_t lanes_of(int s) {
         uint64_t m = 0;
         for (int j = 0; j < GPW; ++j) m |= 1ull << (j * R + s);
@@ -602,14 +616,18 @@ struct Stepper {
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;
         if (chk) {                                                        // wave-uniform
-            const uint32_t ck = c.gbits(chk);
+            // bit q of the group's acks, pre-shifted so that one v_bcnt adds
+            // it (as 16 << q) to the popcount: pc >= (16 << q) + MAJ tests
+            // "response q acked and count >= majority" in one compare
+            const uint32_t ck16 = c.gbits(chk) << 4;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 if (!(chk & L::lanes_of(q))) continue;                    // wave-uniform
-                const int32_t cur = c.r <= q ? n.mc : mc_old;             // rows after / before response q
+                const int32_t cur = ib(L::lanes_upto(q)) ? n.mc : mc_old; // rows after / before response q
                 const uint32_t gt = c.gbits(lm(cur > C));                 // :161
-                const uint64_t inc = lm((ck >> q) & 1u) & lm(__popc(gt) >= MAJ);   // :162 (whole groups)
-                C += ib(inc) ? 1 : 0;
+                const uint32_t pc = __popc(gt) + (ck16 & (16u << q));
+                const uint64_t inc = lm(pc >= (16u << q) + MAJ);          // :162 (whole groups)
+                C = inc_if(C, inc);
                 cnt.add(inc & L::lanes_of(q), RAFT_C_COMMITS);
             }
         }
@@ -700,7 +718,7 @@ struct Stepper {
             const uint64_t endel = bo_end & ~restart;
             const uint64_t sr = start_fire | restart;                       // round head :191-199
             const bool bsr = ib(sr), bend = ib(endel);
-            n.term += bsr ? 1 : 0;                                          // :192
+            n.term = inc_if(n.term, sr);                                    // :192
             n.voted = bsr ? r + 1 : n.voted;                                // :193
             const uint32_t fr = (f & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
                                 (ALL << PEND_SH) | (ib(start_fire) ? FL_ELECTING : 0u);
@@ -852,7 +870,7 @@ struct Stepper {
                                 lm(lead != 0);
             const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
             append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
-            n.cmdc += ib(cm) ? 1 : 0;
+            n.cmdc = inc_if(n.cmdc, cm);
         }
 
         c.clk.mark(PH_C);
