@@ -40,12 +40,31 @@ REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
 GROUP_BYTES = 4 * 3
 
 
-def algorithmic_bytes(c: np.ndarray, G: int, R: int, launches: int) -> float:
-    """Algorithmic HBM bytes of `launches` step-kernel launches over the
-    counted steps, a LOWER bound: the group state is read and
-    written once per launch and every log entry a handler or appendCommand
-    stores is written (8 B).  Log reads are not counted: the register-resident
-    tail cache answers the steady-state ones, and the rest are rare."""
+def algorithmic_bytes(c: np.ndarray, G: int, R: int) -> float:
+    """SURVEY.md §8(d)'s algorithmic HBM bytes of the counted group-steps (the
+    contract's per-unit figure x the units processed):
+
+        B = 2·R·37 + 2·8R·H + 4·P_L + 8·E_L + 4·P_F + 8·E_W + 4·V + 8·C  per group-step
+
+    37 B of canonical scalar state per replica read and written every step,
+    the leader sessions that ticked (H, 2R int32 each, read and written),
+    prevLogTerm reads at the leader (P_L) and follower (P_F), entries read at
+    the leader (E_L) and written at the follower (E_W), last-log-term reads of
+    the vote path (V) and client commands appended (C).  Every event count is
+    the kernel's own counter, summed over the steps of `c`."""
+    ix = abi.C_INDEX
+    s = lambda n: float(c[:, ix[n]].sum())  # noqa: E731
+    return (2.0 * R * 37 * G * c.shape[0] + 2 * 8 * R * s("sessions_ticked")
+            + 4 * s("prev_reads_leader") + 8 * s("entry_reads_leader") + 4 * s("prev_reads_follower")
+            + 8 * s("entry_writes") + 4 * s("vote_log_reads") + 8 * s("commands"))
+
+
+def state_crossing_bytes(c: np.ndarray, G: int, R: int, launches: int) -> float:
+    """The bytes a launch of THIS kernel must move, a lower
+    bound: the group state (fields, tail cache, primary-session column, harness
+    words) read and written once per launch, plus every log entry a handler or
+    appendCommand stores.  A fused launch carries the state across its K steps
+    in VGPRs, so this is far below the algorithmic bytes of its K steps."""
     ix = abi.C_INDEX
     state = 2.0 * G * (R * REPLICA_BYTES + GROUP_BYTES) * launches
     log = 8.0 * (c[:, ix["entry_writes"]].sum() + c[:, ix["commands"]].sum())
@@ -220,9 +239,12 @@ def main():
     if world > 1:
         # the all-reduced counters are global; scale to this rank's share
         local_counts = c_all * (G_local / total_groups)
-    bytes_alg = algorithmic_bytes(local_counts, G_local, R, launches)
     kern_avg_ms = kern_ms / max(1, launches)
-    achieved = bytes_alg / launches / (kern_avg_ms / 1e3) / 1e9 if launches else 0.0
+    kern_s = kern_ms / 1e3
+    bytes_alg = algorithmic_bytes(local_counts, G_local, R)
+    bytes_state = state_crossing_bytes(local_counts, G_local, R, launches)
+    achieved = bytes_alg / kern_s / 1e9 if launches else 0.0
+    achieved_state = bytes_state / kern_s / 1e9 if launches else 0.0
     overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
     K = spl or 1
     tr = load_traffic({"config": args.config, "groups": G_local, "steps_per_launch": K})
@@ -241,12 +263,16 @@ def main():
         eng.set_kernel_timing(False)
         cs = sc.cpu().numpy()[:, : abi.NUM_COUNTERS]
         s_avg = s_ms / max(1, s_n)
-        s_bytes = algorithmic_bytes(cs, G_local, R, s_n) / max(1, s_n)
+        s_bytes = algorithmic_bytes(cs, G_local, R) / max(1, s_n)
+        s_state = state_crossing_bytes(cs, G_local, R, s_n) / max(1, s_n)
         s_ach = s_bytes / (s_avg / 1e3) / 1e9
         s_tr = load_traffic({"config": args.config, "groups": G_local, "steps_per_launch": 1})
         stream = {"steps_per_launch": 1, "steps": args.stream_steps, "kernel_avg_ms": s_avg,
                   "alg_bytes_per_launch": s_bytes, "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": s_ach / HBM_PEAK_GBS, "traffic": s_tr["bytes_per_launch"] if s_tr else None,
+                  "state_bytes_per_launch": s_state,
+                  "achieved_state_crossing": s_state / (s_avg / 1e3) / 1e9,
+                  "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
                   "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
     # ---- safety flags (untimed): the run's counter-borne flags plus the
@@ -291,10 +317,17 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
             "kernel": f"step_kernel<{R}> x{K} fused steps", "kernel_avg_ms": kern_avg_ms, "launches": launches,
             "alg_bytes_per_launch": bytes_alg / max(1, launches),
+            "alg_bytes_per_group_step": bytes_alg / max(1, G_local * local_counts.shape[0]),
             "traffic_source": tr["source"] if tr else None,
-            "note": "fused launches keep every replica in VGPRs for K steps, so HBM carries the state "
-                    "once per K steps and the kernel is VALU-issue bound; roofline_streaming is the "
-                    "same step at one step per launch (HBM-bound formulation)",
+            "state_bytes_per_launch": bytes_state / max(1, launches),
+            "achieved_state_crossing": achieved_state,
+            "frac_state_crossing": achieved_state / HBM_PEAK_GBS,
+            "note": "achieved = SURVEY.md §8(d) algorithmic bytes per group-step (event counts from the "
+                    "kernel's counters) x the group-steps of one launch / the launch's average duration. "
+                    "A fused launch keeps every replica in VGPRs for its K steps, so the HBM bytes it really "
+                    "moves (traffic, PMC) are far below the algorithmic bytes and the kernel is "
+                    "VALU-issue bound; achieved_state_crossing prices only the state a launch must move. "
+                    "roofline_streaming is the same step at one step per launch",
         },
         "roofline_streaming": stream,
         "valid": overflow == 0,

@@ -62,6 +62,15 @@ extern "C" {
 #define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */
 #define RAFT_CMD_ALL_LEADERS   1   /* appendCommand on every LEADER          */
 
+/* ---- protocol modes ---------------------------------- */
+#define RAFT_MODE_REFERENCE 0   /* the reference's handlers, quirks Q1-Q14 included (parity) */
+#define RAFT_MODE_TEXTBOOK  1   /* opt-in, not the reference: append() rejects a stale term,
+                                 * truncates only on conflict and advances the follower commit
+                                 * after the consistency check; a new leader starts at
+                                 * nextIndex = lastIndex + 1; an acked entry sets
+                                 * matchIndex = its index; the leader commit is the median of
+                                 * matchIndex[] with a current-term guard */
+
 /*
  * Engine parameters.  The *_ms defaults are the reference's hard-coded
  * constants; raft_params_default() fills them in.
@@ -90,7 +99,8 @@ typedef struct raft_params {
     int32_t  cmd_mode;          /* RAFT_CMD_*                                                       */
     int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
     int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch, 0..RAFT_MAX_STEPS_PER_LAUNCH (0 = 1) */
-    int32_t  reserved[7];
+    int32_t  mode;              /* RAFT_MODE_* (0 = the reference)                                  */
+    int32_t  reserved[6];
 } raft_params;
 
 /* ---- per-step counters (sum over the engine's groups) ------------------ */

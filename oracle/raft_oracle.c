@@ -33,6 +33,7 @@ typedef struct {
     int32_t  size;        /* Commons.kt:51  mutableListOf<T>() physical size      */
     int32_t  alloc;
     int32_t  cap;         /* build-side physical capacity; overflow counted       */
+    int32_t  textbook;    /* RAFT_MODE_TEXTBOOK: array semantics, no ghost tail   */
     entry_t* items;
 } olog_t;
 
@@ -60,6 +61,15 @@ static int olog_reserve(olog_t* l, int32_t n) {
 /* Commons.kt:56-68.  Returns 1 (true), 0 (false), -1 (build-side overflow:
  * no physical slot left, nothing changes), -2 (ArrayList.set threw, i < 0). */
 static int olog_add(olog_t* l, int32_t i, entry_t e) {
+    if (l->textbook && i >= 0 && i <= l->lastIndex) {
+        /* textbook mode: an array log -- slot i, truncating after it (no ghost tail, Q1) */
+        if (i >= l->cap) return -1;
+        olog_reserve(l, i + 1);
+        l->items[i] = e;
+        l->lastIndex = i + 1;
+        if (l->size < i + 1) l->size = i + 1;      /* high-water mark of written slots */
+        return 1;
+    }
     if (l->lastIndex == i) {                       /* :58 */
         if (l->size >= l->cap) return -1;          /* capacity exhausted: counted, never wrapped */
         olog_reserve(l, l->size + 1);
@@ -205,7 +215,9 @@ static void offer_follower(const ctx_t* x, onode_t* n) {
 static void start_session(const ctx_t* x, onode_t* n) {
     n->hbActive = 1;
     for (int d = 0; d < x->o->R; ++d) {
-        n->nextIndex[d] = n->commitIndex + 1;      /* :112 */
+        n->nextIndex[d] = x->o->p.mode == RAFT_MODE_TEXTBOOK
+                              ? n->log.lastIndex + 1      /* textbook: the leader's next slot */
+                              : n->commitIndex + 1;       /* :112 (Q8) */
         n->matchIndex[d] = 0;                      /* :113 */
     }
     x->c[RAFT_C_LEADERS_ELECTED]++;
@@ -256,7 +268,30 @@ static void end_election(const ctx_t* x, onode_t* n) {
 /* override suspend fun vote(request) (RaftServer.kt:228-251) */
 static void vote_handler(const ctx_t* x, onode_t* n, const raft_vote_req* rq, raft_vote_resp* rs) {
     int granted;
-    if (rq->term < n->currentTerm) granted = 0;                              /* :229 */
+    if (x->o->p.mode == RAFT_MODE_TEXTBOOK) {
+        /* textbook: a higher term is adopted whatever the answer (the reference
+         * adopts it only on a grant, Q5); grant iff votedFor is free or the
+         * candidate and the candidate's log is at least as up to date */
+        if (rq->term > n->currentTerm) {
+            n->currentTerm = rq->term;
+            n->votedFor = -1;
+            if (n->state != RAFT_FOLLOWER) { n->state = RAFT_FOLLOWER; send_follower(x, n); }
+        }
+        granted = 0;
+        if (rq->term == n->currentTerm && (n->votedFor == -1 || n->votedFor == rq->candidate_id)) {
+            entry_t last = { 0, 0 };
+            if (n->log.lastIndex >= 1) {
+                olog_get(&n->log, n->log.lastIndex - 1, &last);
+                x->c[RAFT_C_VOTE_LOG_READS]++;
+            }
+            granted = !(n->log.lastIndex >= 1 && (rq->last_log_term < last.term ||
+                        (rq->last_log_term == last.term && rq->last_log_index < n->log.lastIndex)));
+            if (granted) {                         /* a grant re-arms the timer (:241); the self-vote changes nothing */
+                n->votedFor = rq->candidate_id;
+                if (rq->candidate_id != n->id) send_follower(x, n);
+            }
+        }
+    } else if (rq->term < n->currentTerm) granted = 0;                       /* :229 */
     else if (n->currentTerm == rq->term) granted = (n->votedFor == rq->candidate_id); /* :230 */
     else {
         entry_t last = { 0, 0 };
@@ -283,6 +318,11 @@ static void vote_handler(const ctx_t* x, onode_t* n, const raft_vote_req* rq, ra
 /* override suspend fun append(request) (RaftServer.kt:253-287).
  * Returns 0, or 1 where the reference throws (Log index < -1). */
 static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq, raft_append_resp* rs) {
+    const int tb = x->o->p.mode == RAFT_MODE_TEXTBOOK;
+    if (tb && rq->term < n->currentTerm) {         /* textbook: a stale leader is refused, nothing changes */
+        rs->term = n->currentTerm; rs->success = 0; rs->status = 0;
+        return 0;
+    }
     if (rq->term > n->currentTerm) {               /* :257-262 */
         n->currentTerm = rq->term;
         n->votedFor = -1;
@@ -293,7 +333,7 @@ static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq,
         n->state = RAFT_FOLLOWER;
         send_follower(x, n);
     }
-    if (rq->leader_commit > n->commitIndex) {      /* :270-272 (Q4) */
+    if (!tb && rq->leader_commit > n->commitIndex) {   /* :270-272 (Q4) */
         int32_t c = rq->leader_commit < n->log.lastIndex ? rq->leader_commit : n->log.lastIndex;
         if (c < n->commitIndex) x->c[RAFT_C_COMMIT_REGRESSIONS]++;
         n->commitIndex = c;
@@ -309,11 +349,23 @@ static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq,
         x->c[RAFT_C_PREV_READS_FOLLOWER]++;
         success = (pe.term == rq->prev_log_term);
     } else success = 0;
+    int stored = 0;                                /* the entry is in the log at prev + 1 */
     if (success && rq->has_entry) {                /* :278 (Q2, Q10) */
-        entry_t e = { rq->entry_term, rq->entry_cmd };
-        int r = olog_add(&n->log, rq->prev_log_index + 1, e);
-        if (r == 1) x->c[RAFT_C_ENTRY_WRITES]++;
-        else if (r == -1) x->c[RAFT_C_LOG_OVERFLOW]++;
+        entry_t e = { rq->entry_term, rq->entry_cmd }, cur;
+        const int32_t i = rq->prev_log_index + 1;
+        if (tb && i < n->log.lastIndex && olog_get(&n->log, i, &cur) && cur.term == e.term) {
+            stored = 1;                            /* textbook: no conflict, no truncation */
+        } else {
+            int r = olog_add(&n->log, i, e);
+            if (r == 1) { x->c[RAFT_C_ENTRY_WRITES]++; stored = 1; }
+            else if (r == -1) x->c[RAFT_C_LOG_OVERFLOW]++;
+        }
+    }
+    if (tb && success && rq->leader_commit > n->commitIndex) {
+        /* textbook: commitIndex = min(leaderCommit, index of the last new entry), never lowered */
+        const int32_t lastNew = rq->prev_log_index + 1 + stored;
+        const int32_t c = rq->leader_commit < lastNew ? rq->leader_commit : lastNew;
+        if (c > n->commitIndex) n->commitIndex = c;
     }
     rs->term = n->currentTerm;                     /* :282-285 */
     rs->success = success;
@@ -335,6 +387,7 @@ static void append_command(const ctx_t* x, onode_t* n, uint32_t cmd) {
 static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32_t t, int64_t* c) {
     const raft_params* p = &o->p;
     const int32_t R = o->R, maj = o->majority, P = p->heartbeat_ms;
+    const int tb = p->mode == RAFT_MODE_TEXTBOOK;
     ctx_t x = { o, t, gid, c, -1, 0 };
 
     /* ---- H: harness ---- */
@@ -394,6 +447,7 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
         onode_t* cand = &g->n[s];
         if (!cand->sendMask) continue;
         raft_vote_req rq = { cand->reqTerm, cand->id, cand->reqLastIndex, cand->reqLastTerm };
+        int32_t hiT = 0;
         dropu_t u;
         if (p->drop_ppm) drop_uniforms(&x, RAFT_RNG_VOTE_DROP, s, &u);
         for (int d = 0; d < R; ++d) {
@@ -404,11 +458,18 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
             if (lost(&x, &u, s, d, 1)) { c[RAFT_C_MSG_DROPPED]++; continue; }
             cand->pending &= ~(1u << d);
             cand->latch++;                                          /* :209 countDown() */
-            if (cand->currentTerm < rs.term) cand->state = RAFT_FOLLOWER;  /* :210 (Q6) */
+            if (cand->currentTerm < rs.term) {
+                cand->state = RAFT_FOLLOWER;                        /* :210 (Q6) */
+                if (rs.term > hiT) hiT = rs.term;
+            }
             if (rs.vote_granted) cand->votes++;                     /* :211 */
         }
         cand->sendMask = 0;
         if (cand->pending) cand->retryMs = p->retry_ms;
+        if (tb && hiT > cand->currentTerm) {       /* textbook: adopt the highest response term once the */
+            cand->currentTerm = hiT;               /* round's responses are in (the reference keeps it, Q6) */
+            cand->votedFor = -1;
+        }
     }
 
     /* ---- D: latch closes -> decision (RaftServer.kt:214-222) ---- */
@@ -464,6 +525,8 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
         }
         dropu_t u;
         if (p->drop_ppm) drop_uniforms(&x, RAFT_RNG_APPEND_DROP, s, &u);
+        int stepped = 0;
+        int32_t T = L->currentTerm;                /* textbook: the running response term */
         for (int d = 0; d < R; ++d) {
             if (!ok[d]) continue;
             c[RAFT_C_APPEND_SENT]++;
@@ -471,14 +534,24 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
             raft_append_resp rs;
             if (append_handler(&x, &g->n[d], &rq[d], &rs)) continue;
             if (lost(&x, &u, s, d, 1)) { c[RAFT_C_MSG_DROPPED]++; continue; }
-            if (rs.term > L->currentTerm) {        /* :146-154 (Q7: votedFor kept) */
+            if (tb && rs.term > T) {               /* textbook: adopted after the tick's responses */
+                T = rs.term;
+                stepped = 1;
+                continue;
+            }
+            if (!tb && rs.term > L->currentTerm) { /* :146-154 (Q7: votedFor kept) */
                 L->currentTerm = rs.term;
                 L->state = RAFT_FOLLOWER;
+                stepped = 1;
                 offer_follower(&x, L);
                 continue;                          /* return@launch: only this coroutine */
             }
             if (rs.success) {                      /* :156-165 (Q9) */
-                if (rq[d].has_entry) {
+                if (rq[d].has_entry && tb) {       /* textbook: matchIndex = the acked entry's index */
+                    L->nextIndex[d] += 1;
+                    L->matchIndex[d] = rq[d].prev_log_index + 2;
+                    c[RAFT_C_ENTRIES_ACKED]++;
+                } else if (rq[d].has_entry) {
                     L->nextIndex[d] += 1;
                     L->matchIndex[d] += 1;
                     c[RAFT_C_ENTRIES_ACKED]++;
@@ -490,6 +563,27 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
                 }
             } else {
                 L->nextIndex[d] -= 1;              /* :167 */
+            }
+        }
+        if (tb && stepped) {                       /* the higher term, FOLLOWER, a new term's empty vote */
+            L->currentTerm = T;
+            L->state = RAFT_FOLLOWER;
+            L->votedFor = -1;
+            offer_follower(&x, L);
+        }
+        if (tb && !stepped) {
+            /* textbook commit rule: N = the majority-th largest matchIndex (the
+             * median of the session row); commit up to N iff log[N-1] is of the
+             * leader's current term.  COMMITS counts the ticks that advanced. */
+            int32_t m[MAXR];
+            for (int k = 0; k < R; ++k) m[k] = L->matchIndex[k];
+            for (int a = 1; a < R; ++a)            /* insertion sort, descending */
+                for (int b = a; b > 0 && m[b] > m[b - 1]; --b) { int32_t v = m[b]; m[b] = m[b - 1]; m[b - 1] = v; }
+            const int32_t N = m[maj - 1];
+            entry_t ne;
+            if (N > L->commitIndex && olog_get(&L->log, N - 1, &ne) && ne.term == L->currentTerm) {
+                L->commitIndex = N;
+                c[RAFT_C_COMMITS]++;
             }
         }
     }
@@ -531,13 +625,15 @@ static void init_group(const struct oracle* o, ogroup_t* g, uint32_t gid) {
         n->votedFor = -1;                          /* :39 */
         n->state = RAFT_FOLLOWER;                  /* :42 */
         n->log.cap = o->p.log_cap;
+        n->log.textbook = o->p.mode == RAFT_MODE_TEXTBOOK;
         reset_timer(&x, n);                        /* init: ResettableCountdownTimer(...) starts (:58, Commons.kt:14) */
     }
 }
 
 int oracle_create(const raft_params* p, oracle_t** out) {
     if (!p || !out || p->R < 1 || p->R > MAXR || p->G < 1 || p->log_cap < 1 || p->heartbeat_ms <= 0 ||
-        p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms)
+        p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms ||
+        (p->mode != RAFT_MODE_REFERENCE && p->mode != RAFT_MODE_TEXTBOOK))
         return RAFT_EINVAL;
     oracle_t* o = (oracle_t*)calloc(1, sizeof(*o));
     if (!o) return RAFT_ENOMEM;

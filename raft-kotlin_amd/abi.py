@@ -29,6 +29,8 @@ MAX_R = 8
 
 CMD_LOWEST_LEADER = 0
 CMD_ALL_LEADERS = 1
+MODE_REFERENCE = 0
+MODE_TEXTBOOK = 1
 
 COUNTER_NAMES = [
     "leaders", "groups_with_leader", "timeouts", "rounds", "votes_granted",
@@ -64,7 +66,7 @@ class raft_params(C.Structure):
         ("drop_ppm", C.c_uint32), ("churn_ppm", C.c_uint32), ("churn_steps", C.c_int32),
         ("partition_period", C.c_int32), ("partition_len", C.c_int32),
         ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
-        ("steps_per_launch", C.c_int32), ("reserved", C.c_int32 * 7),
+        ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("reserved", C.c_int32 * 6),
     ]
 
 

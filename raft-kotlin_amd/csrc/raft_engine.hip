@@ -151,7 +151,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 #ifndef RAFT_STEP_WAVES_PER_EU
 #define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
 #endif
-template <int R>
+template <int R, bool TB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
@@ -212,7 +212,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         }
         Counters cnt;
         cnt.clear();
-        Stepper<R>::step(p, c, n, cnt);
+        Stepper<R, TB>::step(p, c, n, cnt);
         c.clk.mark(PH_TDRAW);
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
@@ -455,6 +455,7 @@ __device__ __forceinline__ void resolve_rep_draw(RepState& x, const DevParams& p
 enum { BATCH_VOTE = 0, BATCH_APPEND = 1, BATCH_COMMAND = 2 };
 
 // keys[k] = group * R + replica; msgs of key k are order[off[k] .. off[k+1])
+template <bool TB>
 __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int nkeys,
                                                       const int64_t* keys, const int64_t* off, const int64_t* order,
                                                       const void* req, void* resp) {
@@ -476,7 +477,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
             uint64_t gr;
-            vote_handler(x.ref(), __ballot(1), q.term, q.candidate_id, q.last_log_index, q.last_log_term, cnt, rt, gr);
+            vote_handler<TB>(x.ref(), __ballot(1), r + 1, q.term, q.candidate_id, q.last_log_index, q.last_log_term,
+                             cnt, rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
@@ -484,13 +486,14 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             uint64_t su = 0;
             const int32_t pv = q.prev_log_index;
             const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lr[pv].x : 0;
-            const uint64_t thrown = append_handler(x.ref(), __ballot(1), r + 1, lr, p.cap, q.term, q.leader_id, pv,
-                                                   q.prev_log_term, __ballot(q.has_entry != 0),
-                                                   Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, cnt, rt,
-                                                   su);
+            const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lr[pv + 1].x : 0;
+            const uint64_t thrown = append_handler<TB>(x.ref(), __ballot(1), r + 1, lr, p.cap, q.term, q.leader_id, pv,
+                                                       q.prev_log_term, __ballot(q.has_entry != 0),
+                                                       Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
+                                                       cnt, rt, su);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
-            append_command(x.ref(), __ballot(1), lr, p.cap, ((const uint32_t*)req)[o], cnt);
+            append_command<TB>(x.ref(), __ballot(1), lr, p.cap, ((const uint32_t*)req)[o], cnt);
         }
         resolve_rep_draw(x, p, t, gid, r);
     }
@@ -545,7 +548,11 @@ template <int R> struct InitL {
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
-        step_kernel<R><<<e->nblocks, BLOCK, (size_t)k * WAVES_PER_BLOCK * NCW * 4, e->stream>>>(e->dp, t0, k,
+        const size_t lds = (size_t)k * WAVES_PER_BLOCK * NCW * 4;
+        if (e->p.mode == RAFT_MODE_TEXTBOOK)
+            step_kernel<R, true><<<e->nblocks, BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
+        else
+            step_kernel<R, false><<<e->nblocks, BLOCK, lds, e->stream>>>(e->dp, t0, k,
                                                                                              e->partials);
     }
 };
@@ -619,6 +626,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_EINVAL, "steps_per_launch must be in 0..RAFT_MAX_STEPS_PER_LAUNCH");
     if (p->heartbeat_ms <= 0 || p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms)
         return fail(RAFT_EINVAL, "bad timer constants");
+    if (p->mode != RAFT_MODE_REFERENCE && p->mode != RAFT_MODE_TEXTBOOK)
+        return fail(RAFT_EINVAL, "mode must be RAFT_MODE_REFERENCE or RAFT_MODE_TEXTBOOK");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RAFT_ENODEV, "no HIP device");
     if (device < 0 || device >= ndev) return fail(RAFT_EINVAL, "bad device index");
@@ -957,7 +966,8 @@ static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32
     if (err == hipSuccess) err = hipMemcpyAsync(pd, order.data(), b_ord, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(pq, req, b_req, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) {
-        batch_kernel<<<(nk + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
+        auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true> : batch_kernel<false>;
+        kern<<<(nk + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
             e->dp, (uint32_t)e->t, kind, nk, (const int64_t*)pk, (const int64_t*)po, (const int64_t*)pd, pq,
             resp_sz ? (void*)ps : nullptr);
         err = hipGetLastError();

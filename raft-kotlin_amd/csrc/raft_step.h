@@ -206,12 +206,16 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
 //   i == lastIndex: :58-61, log.add(entry) appends at the PHYSICAL end (Q1);
 //   i <  lastIndex: :63-66, log[i] = entry, lastIndex = i + 1, no shrink.
 // The build refuses an append beyond log_cap (counted, never wrapped).
+//
+// TB (RAFT_MODE_TEXTBOOK): an array log instead -- slot i is written and
+// everything after it dropped (no ghost tail); physLen is the high-water mark.
+template <bool TB = false>
 __device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
                                         uint64_t& overflow) {
     const int32_t last = n.last, phys = n.phys;
     const uint64_t app = lm(i == last);
-    const uint64_t ghost = app & lm(phys != last);     // the stale slot log[last] becomes the last entry
-    overflow = act & app & lm(phys >= cap);
+    const uint64_t ghost = TB ? 0ull : app & lm(phys != last);   // the stale slot log[last] becomes the last entry
+    overflow = TB ? act & lm(i >= cap) : act & app & lm(phys >= cap);
     wrote = act & ~overflow;
     // the one slot the new tail cache needs from HBM
     const uint64_t ld = wrote & (ghost | (lm(i != last) & lm(i >= 1) & lm(i != last - 1)));
@@ -232,18 +236,40 @@ __device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, En
         }
     }
     const bool w = ib(wrote);
-    if (w) lr[ap ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
+    if (w) lr[(ap && !TB) ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
     n.t1 = w ? t1 : n.t1;
     n.c1 = w ? c1 : n.c1;
     n.t2 = w ? t2 : n.t2;
-    n.phys = ib(wrote & app) ? phys + 1 : phys;
+    if constexpr (TB) n.phys = w ? max(phys, i + 1) : phys;
+    else n.phys = ib(wrote & app) ? phys + 1 : phys;
     n.last = w ? i + 1 : last;
 }
 
 // ---- vote() (RaftServer.kt:228-251), applied on the lanes of act ----------
-template <class CNT>
-__device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t rt, int32_t rc, int32_t rli, int32_t rlt,
-                                             CNT& cnt, int32_t& resp_term, uint64_t& granted) {
+template <bool TB, class CNT>
+__device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, int32_t rt, int32_t rc, int32_t rli,
+                                             int32_t rlt, CNT& cnt, int32_t& resp_term, uint64_t& granted) {
+    if constexpr (TB) {
+        // textbook: a higher term is adopted whatever the answer (Q5 adopts it
+        // only on a grant); grant iff votedFor is free or the candidate and the
+        // candidate's log is at least as up to date; the self-vote changes nothing
+        const uint64_t higher = act & lm(rt > n.term);
+        const bool h = ib(higher);
+        n.fl |= ib(higher & lm(n.role != RAFT_FOLLOWER)) ? follower_sent(n.fl) : 0u;
+        n.term = h ? rt : n.term;
+        n.voted = h ? -1 : n.voted;
+        n.role = h ? (int32_t)RAFT_FOLLOWER : n.role;
+        const uint64_t elig = act & lm(rt == n.term) & (lm(n.voted == -1) | lm(n.voted == rc));
+        const uint64_t hasl = lm(n.last >= 1);
+        const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));
+        granted = elig & ~logrej;
+        cnt.add(elig & hasl, RAFT_C_VOTE_LOG_READS);
+        cnt.add(granted, RAFT_C_VOTES_GRANTED);
+        n.voted = ib(granted) ? rc : n.voted;
+        n.fl |= ib(granted & lm(rc != id)) ? follower_sent(n.fl) : 0u;
+        resp_term = n.term;
+        return;
+    }
     const uint64_t higher = lm(rt > n.term);                                    // :229-231
     const uint64_t hasl = lm(n.last >= 1);
     const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));   // :232-236 (Q5)
@@ -264,11 +290,18 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t rt, in
 // -1): those calls have no response.  dprev = term of this replica's
 // log[prev], read by the caller ahead of time (valid whenever 0 <= prev <
 // lastIndex).
-template <class CNT>
+//
+// TB: a request with a stale term is refused with no state change; the entry
+// is written only if the slot is absent or holds another term (dnext = term of
+// this replica's log[prev+1], valid whenever 0 <= prev+1 < lastIndex); the
+// commit follows leaderCommit only after the consistency check, up to the last
+// entry the request vouches for, and never goes down.
+template <bool TB, class CNT>
 __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, uint2* lr, int cap, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
-                                                   Entry e, int32_t lcommit, int32_t dprev, CNT& cnt,
+                                                   Entry e, int32_t lcommit, int32_t dprev, int32_t dnext, CNT& cnt,
                                                    int32_t& resp_term, uint64_t& success) {
+    if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
     const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
     const bool u = ib(up), f = ib(fol);
@@ -276,27 +309,36 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
     n.term = u ? rt : n.term;
     n.voted = u ? -1 : n.voted;
     n.role = f ? (int32_t)RAFT_FOLLOWER : n.role;
-    const uint64_t cu = act & lm(lcommit > n.commit);                           // :270-272 (Q4)
-    const int32_t cc = min(lcommit, n.last);
-    cnt.add(cu & lm(cc < n.commit), RAFT_C_COMMIT_REGRESSIONS);
-    n.commit = ib(cu) ? cc : n.commit;
+    if constexpr (!TB) {
+        const uint64_t cu = act & lm(lcommit > n.commit);                       // :270-272 (Q4)
+        const int32_t cc = min(lcommit, n.last);
+        cnt.add(cu & lm(cc < n.commit), RAFT_C_COMMIT_REGRESSIONS);
+        n.commit = ib(cu) ? cc : n.commit;
+    }
     const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
     const uint64_t thrown = check & lm(prev < 0);
     cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
     success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
     uint64_t wrote, ovf;
-    log_add(lr, cap, n, prev + 1, e, success & has, wrote, ovf);                // :278 (Q2, Q10)
+    uint64_t same = 0;                                                          // TB: entry already there
+    if constexpr (TB) same = success & has & lm(prev + 1 < n.last) & lm(dnext == e.term);
+    log_add<TB>(lr, cap, n, prev + 1, e, success & has & ~same, wrote, ovf);    // :278 (Q2, Q10)
     cnt.add(wrote, RAFT_C_ENTRY_WRITES);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
+    if constexpr (TB) {
+        const int32_t lastNew = prev + 1 + (ib(wrote | same) ? 1 : 0);
+        const int32_t cc = max(n.commit, min(lcommit, lastNew));
+        n.commit = ib(success & lm(lcommit > n.commit)) ? cc : n.commit;
+    }
     resp_term = n.term;                                                         // :282-285
     return thrown;
 }
 
 // ---- appendCommand() (RaftServer.kt:100-107), applied on the lanes of act -
-template <class CNT>
+template <bool TB, class CNT>
 __device__ __forceinline__ void append_command(Rep n, uint64_t act, uint2* lr, int cap, uint32_t cmd, CNT& cnt) {
     uint64_t wrote, ovf;
-    log_add(lr, cap, n, n.last, Entry{n.term, cmd}, act, wrote, ovf);
+    log_add<TB>(lr, cap, n, n.last, Entry{n.term, cmd}, act, wrote, ovf);
     cnt.add(act, RAFT_C_COMMANDS);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
 }
@@ -455,7 +497,9 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
     }
 }
 
-template <int R>
+// TB: RAFT_MODE_TEXTBOOK (include/raft_engine.h), compiled as its own kernel
+// so the reference-parity kernel carries none of it.
+template <int R, bool TB>
 struct Stepper {
     using L = Lanes<R>;
     static constexpr int MAJ = L::MAJ;
@@ -500,7 +544,7 @@ struct Stepper {
 #pragma unroll
         for (int s = 0; s < R; ++s) {
             if (!(starting & L::lanes_of(s))) continue;                   // wave-uniform
-            const int32_t cs = bcast(n.commit, c.src(s));
+            const int32_t cs = bcast(TB ? n.last : n.commit, c.src(s));  // TB: nextIndex = lastIndex + 1
             const uint64_t mst = lm((sb >> s) & 1u);
             const uint64_t msp = mst & lm(n.s0 >= 0) & lm(n.s0 != s);
             if (msp) {
@@ -508,7 +552,7 @@ struct Stepper {
             }
             const bool st = ib(mst);
             n.s0 = st ? s : n.s0;
-            n.nx = st ? cs + 1 : n.nx;                                    // :112
+            n.nx = st ? cs + 1 : n.nx;                                    // :112 (Q8)
             n.mc = st ? 0 : n.mc;                                         // :113
         }
     }
@@ -561,15 +605,18 @@ struct Stepper {
         const uint2* ls = c.lr + (int64_t)(s - c.r) * p.cap;
         int32_t lpt = cached_term(Llast, Lt1, Lt2, prev);
         int32_t dpt = cached_term(n.last, n.t1, n.t2, prev);
+        int32_t dnt = TB ? cached_term(n.last, n.t1, n.t2, prev + 1) : 0;  // TB: own log[prev+1]
         uint2 lent = make_uint2((uint32_t)Lt1, Lc1);
         const uint64_t ld1 = ok & p0 & lm(prev < Llast - 2);
         const uint64_t ld2 = run & has & lm(i < Llast);
         const uint64_t ld3 = ok & p0 & lm(prev < n.last - 2);
-        if (ld1 | ld2 | ld3) {                                            // rare: tail-cache misses
+        const uint64_t ld4 = TB ? ok & has & lm(prev + 1 < n.last - 2) : 0ull;
+        if (ld1 | ld2 | ld3 | ld4) {                                      // rare: tail-cache misses
             if (ib(ld1)) lpt = (int32_t)ls[prev].x;
             if (ib(ld2)) lent = ls[i - 1];
             if (ib(ld3)) dpt = (int32_t)c.lr[prev].x;
-            asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt));   // wait inside the branch
+            if (TB && ib(ld4)) dnt = (int32_t)c.lr[prev + 1].x;
+            asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt), "v"(dnt));   // wait inside the branch
         }
 
         // both directions' losses resolved here: a lane mask of comparisons made
@@ -581,8 +628,8 @@ struct Stepper {
         int32_t rterm;
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
-        append_handler(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
-                       Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, cnt, rterm, succ);
+        append_handler<TB>(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
@@ -610,12 +657,12 @@ struct Stepper {
         const uint64_t nak = nd & ~succ;                                  // :166-167
         const bool bchk = ib(chk);
         n.nx += bchk ? 1 : (ib(nak) ? -1 : 0);
-        n.mc = bchk ? mc_old + 1 : (ib(hbk) ? prev + 1 : mc_old);
+        n.mc = bchk ? (TB ? prev + 2 : mc_old + 1) : (ib(hbk) ? prev + 1 : mc_old);   // TB: the entry's index
         cnt.add(chk, RAFT_C_ENTRIES_ACKED);
         // commit rule, after each acknowledged entry in destination order:
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;
-        if (chk) {                                                        // wave-uniform
+        if (!TB && chk) {                                                 // wave-uniform
             // bit q of the group's acks, pre-shifted so that one v_bcnt adds
             // it (as 16 << q) to the popcount: pc >= (16 << q) + MAJ tests
             // "response q acked and count >= majority" in one compare
@@ -631,11 +678,41 @@ struct Stepper {
                 cnt.add(inc & L::lanes_of(q), RAFT_C_COMMITS);
             }
         }
+        if constexpr (TB) {
+            // textbook commit rule: N = the majority-th largest matchIndex of the
+            // session row (a sorting network over the group's R lanes); commit up
+            // to N iff the leader's log[N-1] is of its current term and it did
+            // not step down this tick.  COMMITS counts the ticks that advance.
+            if (run) {                                                    // wave-uniform
+                int32_t v[R];
+#pragma unroll
+                for (int q = 0; q < R; ++q) v[q] = bcast(n.mc, c.src(q));
+#pragma unroll
+                for (int a = 0; a < R; ++a)                               // descending
+#pragma unroll
+                    for (int b = R - 1; b > a; --b) {
+                        const int32_t hi = max(v[b - 1], v[b]), lo = min(v[b - 1], v[b]);
+                        v[b - 1] = hi; v[b] = lo;
+                    }
+                const int32_t N = v[MAJ - 1];
+                const uint64_t cand = run & lm(!stepdown) & lm(N > C) & lm(N <= Llast);
+                int32_t NT = N - 1 == Llast - 1 ? Lt1 : Lt2;
+                const uint64_t ldn = cand & lm(N - 1 < Llast - 2);
+                if (ldn) {
+                    if (ib(ldn)) NT = (int32_t)ls[N - 1].x;
+                    asm volatile("" :: "v"(NT));
+                }
+                const uint64_t adv = cand & lm(NT == Lterm);
+                C = ib(adv) ? N : C;
+                cnt.add(adv & mme, RAFT_C_COMMITS);
+            }
+        }
         const bool wb = ib(run & mme);
         const bool sd = wb && stepdown;                                   // :148 + offer(FOLLOWER) :152 (S-6)
         n.term = wb ? T : n.term;
         n.commit = wb ? C : n.commit;
         n.role = sd ? (int32_t)RAFT_FOLLOWER : n.role;
+        if constexpr (TB) n.voted = sd ? -1 : n.voted;                    // TB: a new term has no vote yet
         n.fl |= (sd && !(n.fl & FL_ELECTING)) ? (FL_ARMED | FL_DRAW) : 0u;
     }
 
@@ -660,7 +737,7 @@ struct Stepper {
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
-        vote_handler(n.rep(), act, rt, s + 1, rli, rlt, cnt, rterm, granted);
+        vote_handler<TB>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, cnt, rterm, granted);
         const uint64_t lresp = act & lost(p, c, s, r, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
@@ -674,6 +751,20 @@ struct Stepper {
         f += (uint32_t)__popc(gr) << VOTES_SH;                      // :211
         n.fl = me ? f : n.fl;
         n.role = (me && hi) ? (int32_t)RAFT_FOLLOWER : n.role;     // :210 (Q6)
+        if constexpr (TB) {
+            // textbook: the candidate adopts the highest response term once its
+            // round's responses are in (the reference keeps its term, Q6)
+            if (lm(hi != 0)) {                                      // wave-uniform, rare
+                int32_t T = st;
+#pragma unroll
+                for (int q = 0; q < R; ++q) {
+                    const int32_t tq = bcast(rterm, c.src(q));
+                    T = ((dl >> q) & 1u) ? max(T, tq) : T;
+                }
+                n.term = (me && hi) ? T : n.term;
+                n.voted = (me && hi) ? -1 : n.voted;
+            }
+        }
         n.retry = (me && ((f >> PEND_SH) & 0xFFu)) ? p.retry : n.retry;
     }
 
@@ -869,7 +960,7 @@ struct Stepper {
             const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
                                 lm(lead != 0);
             const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
-            append_command(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
+            append_command<TB>(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
             n.cmdc = inc_if(n.cmdc, cm);
         }
 

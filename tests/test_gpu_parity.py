@@ -203,6 +203,55 @@ def test_full_size_config3_sampled():
     assert np.all(last <= phys) and np.all(last >= 0)
 
 
+# ---- RAFT_MODE_TEXTBOOK (opt-in, not the reference) ------------
+
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_textbook_lockstep(cfg):
+    """The textbook kernel (step_kernel<R, true>) against the oracle's textbook
+    mode, bit-exact, and its committed prefixes Log-Matching clean."""
+    kw = dict(abi.CONFIGS[cfg], mode=abi.MODE_TEXTBOOK)
+    kw.update({2: dict(G=5_000), 3: dict(G=10_000, churn_ppm=10_000), 5: dict(G=1_000)}[cfg])
+    steps, cap = {2: (400, 200), 3: (1_200, 500), 5: (1_200, 1_400)}[cfg]
+    e, o = pair(log_cap=cap, steps_per_launch=32, **kw)
+    se, ov = run_lockstep(e, o, steps, 100, f"textbook config{cfg}", digest_every=4)
+    assert ov == 0
+    assert check_log_matching(e, o, f"textbook config{cfg}") == 0
+
+
+@pytest.mark.parametrize("R", [1, 2, 4, 7, 8])
+def test_textbook_other_replica_counts(R):
+    e, o = pair(R=R, G=2000, seed=200 + R, log_cap=300, drop_ppm=100_000, churn_ppm=20_000, churn_steps=15,
+                cmd_ppm=500_000, partition_period=40, partition_len=10, mode=abi.MODE_TEXTBOOK)
+    run_lockstep(e, o, 400, 50, f"textbook R={R}")
+    assert check_log_matching(e, o, f"textbook R={R}") == 0
+
+
+FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_size.json")
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_full_size_digest(cfg):
+    """The north star's full-size runs, bit-exact: config 3 (10^6 x 5, 10^4
+    steps) and config 5 (10^5 x 7, 10^4 steps) on the GPU against the oracle's
+    whole-run digest (state, sessions and every physical log slot of every
+    group) and its per-step counters, precomputed on the CPU by
+    tests/golden/make_full_size.py."""
+    import json
+    meta = json.load(open(FULL))[f"c{cfg}"]
+    want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))[f"c{cfg}_counters"]
+    kw = dict(abi.CONFIGS[cfg])
+    assert meta["groups"] == kw["G"] and meta["params"] == {k: v for k, v in kw.items() if k != "G"}
+    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], **kw))
+    ce = e.step(meta["steps"])
+    if not np.array_equal(ce, want):
+        bad = np.argwhere(ce != want)[0]
+        raise AssertionError(f"config {cfg}: counters differ at step {bad[0]} ({abi.COUNTER_NAMES[bad[1]]}): "
+                             f"{ce[tuple(bad)]} vs {want[tuple(bad)]}")
+    assert f"{e.digest():016x}" == meta["digest"], f"config {cfg}: whole-run digest differs"
+    assert ce[:, abi.C_INDEX["log_overflow"]].sum() == 0
+    e.close()
+
+
 # ---- the service boundary: single handlers vs the oracle -------------------------
 
 def random_states(rng, n, R, cap):
@@ -224,11 +273,12 @@ def random_states(rng, n, R, cap):
     return w, logs_t, logs_c
 
 
-def test_handler_batches_vs_oracle():
+@pytest.mark.parametrize("mode", [abi.MODE_REFERENCE, abi.MODE_TEXTBOOK])
+def test_handler_batches_vs_oracle(mode):
     rng = np.random.default_rng(7)
     R, G, cap, n = 5, 64, 8, 3000
     w, lt, lc = random_states(rng, G, R, cap)
-    e, o = pair(R=R, G=G, log_cap=cap, seed=3)
+    e, o = pair(R=R, G=G, log_cap=cap, seed=3, mode=mode)
     for x in (e, o):
         x.write_state(w)
         x.write_log(lt, lc)
