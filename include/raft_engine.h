@@ -62,7 +62,7 @@ extern "C" {
 #define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */
 #define RAFT_CMD_ALL_LEADERS   1   /* appendCommand on every LEADER          */
 
-/* ---- protocol modes ---------------------------------- */
+/* ---- protocol modes -------------------------------- */
 #define RAFT_MODE_REFERENCE 0   /* the reference's handlers, quirks Q1-Q14 included (parity) */
 #define RAFT_MODE_TEXTBOOK  1   /* opt-in, not the reference: append() rejects a stale term,
                                  * truncates only on conflict and advances the follower commit

@@ -203,7 +203,7 @@ def test_full_size_config3_sampled():
     assert np.all(last <= phys) and np.all(last >= 0)
 
 
-# ---- RAFT_MODE_TEXTBOOK (opt-in, not the reference; DESIGN.md §3.12) ------------
+# ---- RAFT_MODE_TEXTBOOK (opt-in, not the reference; DESIGN.md §3 S-14) ------------
 
 @pytest.mark.parametrize("cfg", [2, 3, 5])
 def test_textbook_lockstep(cfg):

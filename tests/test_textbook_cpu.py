@@ -1,4 +1,4 @@
-"""RAFT_MODE_TEXTBOOK (SURVEY.md §8(f) 4, DESIGN.md §3.12) on the CPU oracle.
+"""RAFT_MODE_TEXTBOOK (SURVEY.md §8(f) 4, DESIGN.md §3 S-14) on the CPU oracle.
 
 Textbook mode is opt-in and NOT the reference: it replaces the quirks that
 break Raft's safety properties (Q1 ghost tail, Q2 unconditional truncation,
