@@ -136,6 +136,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
+                    help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
     ap.add_argument("--steps-per-launch", type=int, default=64,
                     help="lockstep steps fused into one kernel launch (state stays in VGPRs)")
     ap.add_argument("--stream-steps", type=int, default=200,
@@ -173,9 +175,12 @@ def main():
         G_local = args.groups // world + (1 if rank < args.groups % world else 0)
         g0 = rank * (args.groups // world) + min(rank, args.groups % world)
     total_steps = args.warmup + args.steps + args.stream_steps
-    log_cap = args.log_cap or int(64 + 0.3 * total_steps)
+    # physical slots a replica can fill: ~0.3 per step at config 3's command
+    # rate, up to one per step where every leader takes a command each step
+    log_cap = args.log_cap or int(64 + (1.0 if kw["cmd_ppm"] >= 1_000_000 else 0.3) * total_steps)
     spl = args.steps_per_launch
-    params = abi.make_params(log_cap=log_cap, steps_per_launch=spl, **dict(kw, G=G_local, g0=g0))
+    mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
+    params = abi.make_params(log_cap=log_cap, steps_per_launch=spl, mode=mode, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
@@ -306,8 +311,10 @@ def main():
         "data": "synthetic (seeded Philox harness: drops, churn, commands)",
         "config": {
             "workload": f"config{args.config}: {G_local} groups/GPU x {R} replicas"
-                        + (", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step"
-                           if args.config == 3 else ""),
+                        + {3: ", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step",
+                           5: ", 2-way partitions 25 of every 50 steps, 1 command per step to every leader",
+                           2: ", no faults, 1/4 command per group-step"}[args.config]
+                        + (", textbook mode" if mode else ""),
             "groups_total": total_groups, "replicas": R, "log_cap": log_cap,
             "steps_per_launch": K, "parallelism": f"shard-by-group x{world}",
             "counter_allreduce_every": args.reduce_every if world > 1 else None,
@@ -335,7 +342,7 @@ def main():
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, kw, log_cap, args.warmup + args.steps)
+        out["cpu_baseline"] = cpu_baseline(args, dict(kw, mode=mode), log_cap, args.warmup + args.steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
