@@ -138,12 +138,13 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
                     help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
-    ap.add_argument("--steps-per-launch", type=int, default=64,
+    ap.add_argument("--steps-per-launch", type=int, default=512,
                     help="lockstep steps fused into one kernel launch (state stays in VGPRs)")
     ap.add_argument("--stream-steps", type=int, default=200,
                     help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
-    ap.add_argument("--reduce-every", type=int, default=256, help="steps per counter all-reduce")
+    ap.add_argument("--reduce-every", type=int, default=512,
+                    help="steps per counter all-reduce (and per step_async call: keep it a multiple of --steps-per-launch)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")

@@ -56,7 +56,7 @@ extern "C" {
 #define RAFT_LEADER    2
 
 #define RAFT_MAX_R 8
-#define RAFT_MAX_STEPS_PER_LAUNCH 128   /* steps fused into one kernel launch (LDS counter rows) */
+#define RAFT_MAX_STEPS_PER_LAUNCH 512   /* steps fused into one kernel launch (LDS counter rows) */
 
 /* ---- command-injection modes (harness) ---------------- */
 #define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */

@@ -41,7 +41,7 @@ COUNTER_NAMES = [
 ]
 NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
-MAX_STEPS_PER_LAUNCH = 128
+MAX_STEPS_PER_LAUNCH = 512
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
 
 FIELD_NAMES = ["term", "voted", "role", "commit", "last", "phys",

@@ -144,10 +144,13 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 }
 
 // K lockstep steps of every group.  A wave holds GPW whole groups, one lane
-// per replica.  Counters: a wave's totals of a step (SGPRs) go to its own LDS
-// row [k][wave][NCW] with one plain store -- no atomic, no wait in the step
-// loop -- and after the loop (the launch's only barrier) the workgroup sums
-// its waves' rows into the partials [k][NCW][nblocks].
+// per replica.  Counters: a wave's totals of a step (SGPRs) are added into the
+// workgroup's LDS row [k][NCW] with one return-less ds_add (no wait in the
+// step loop), and after the loop the workgroup copies its rows into the
+// partials [k][NCW][nblocks].  One row per workgroup (not per wave) keeps the
+// LDS footprint at K * NCW words, so K can reach RAFT_MAX_STEPS_PER_LAUNCH
+// without costing occupancy; the launch's two barriers (zeroing, final copy)
+// sit outside the step loop.
 #ifndef RAFT_STEP_WAVES_PER_EU
 #define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
 #endif
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
     using L = Lanes<R>;
-    extern __shared__ uint32_t lds_cnt[];                                 // [nsteps][WAVES_PER_BLOCK][NCW]
+    extern __shared__ uint32_t lds_cnt[];                                 // [nsteps][NCW]
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     const int wid = blockIdx.x * WAVES_PER_BLOCK + wib;
@@ -178,6 +181,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.job = u32x4{0u, 0u, 0u, 0u};
     c.tw = c.dwt = c.dwv = 0u;
 
+    for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK) lds_cnt[q] = 0u;
     Node n;
     c.clk.start();
     if (live) load_node(n, p, g, idx);
@@ -186,6 +190,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
     // previous step's log stores, so each step would start by waiting for them.
     __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
+    __syncthreads();                                                      // counter rows zeroed
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;
         c.t = t;
@@ -217,17 +222,13 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
         for (int cw = 0; cw < NCW; ++cw) v = (uint32_t)raft_writelane((int32_t)cnt.s[cw], cw, (int32_t)v);
-        if (lane < NCW) lds_cnt[(k * WAVES_PER_BLOCK + wib) * NCW + lane] = v;
+        // < 2^16 per half per workgroup: a wave counts < 2^14 events of a kind per step
+        if (lane < NCW) __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         c.clk.mark(PH_CNT);
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK) {              // workgroup partials
-        const int k = q / NCW, cw = q - k * NCW;
-        uint32_t s = 0;                                                     // < 2^16 per half per block
-#pragma unroll
-        for (int w = 0; w < WAVES_PER_BLOCK; ++w) s += lds_cnt[(k * WAVES_PER_BLOCK + w) * NCW + cw];
-        partials[((int64_t)k * NCW + cw) * gridDim.x + blockIdx.x] = s;
-    }
+    for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK)               // workgroup partials
+        partials[(int64_t)q * gridDim.x + blockIdx.x] = lds_cnt[q];
 #ifdef RAFT_PROFILE_PHASES
     if (lane == 0)
         for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
@@ -548,7 +549,7 @@ template <int R> struct InitL {
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
-        const size_t lds = (size_t)k * WAVES_PER_BLOCK * NCW * 4;
+        const size_t lds = (size_t)k * NCW * 4;
         if (e->p.mode == RAFT_MODE_TEXTBOOK)
             step_kernel<R, true><<<e->nblocks, BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
         else

@@ -7,7 +7,7 @@ rm -f raft-kotlin_amd/lib/libraft_engine_*.so
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I include $flags \
-      -o raft-kotlin_amd/lib/libraft_engine_$name.so raft-kotlin_amd/csrc/raft_engine.hip &
+      -o raft-kotlin_amd/lib/libraft_engine_$name.so raft-kotlin_amd/csrc/raft_engine.hip raft-kotlin_amd/csrc/raft_wire.cpp &
 done
 wait
 ls raft-kotlin_amd/lib/

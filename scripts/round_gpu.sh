@@ -11,9 +11,9 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/smoke.log"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc" | tee -a "$OUT/bench.log"; [ $rc -ne 0 ] && exit $rc
-# kernel-trace of the fused bench (K=64 launches only) and of the streaming form (K=1)
+# kernel-trace of the fused bench (K=512 launches only) and of the streaming form (K=1)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python bench.py --steps 2048 --warmup 64 --stream-steps 0 --no-cpu-baseline > "$OUT/trace.log" 2>&1
+    python bench.py --steps 2048 --warmup 512 --stream-steps 0 --no-cpu-baseline > "$OUT/trace.log" 2>&1
 rc=$?; echo "trace rc=$rc" | tee -a "$OUT/trace.log"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k1" -o run --output-format csv -- \
     python bench.py --steps 512 --warmup 64 --steps-per-launch 1 --stream-steps 0 --no-cpu-baseline \

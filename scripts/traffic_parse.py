@@ -33,8 +33,8 @@ def per_dispatch(d, counter):
     return [v for _, v in sorted(rows)]
 
 
-# scripts/traffic_run.py workload: 2 warmup launches + 4 launches at K=64, then 20 at K=1
-SPLITS = {64: slice(2, 6), 1: slice(6, 26)}
+# scripts/traffic_run.py workload: 2 warmup launches + 4 launches at K=64, 2 at K=512, then 20 at K=1
+SPLITS = {64: slice(2, 6), 512: slice(6, 8), 1: slice(8, 28)}
 
 
 def main(d):

@@ -1,7 +1,7 @@
 """Workloads for the rocprofv3 --pmc traffic passes (scripts/traffic.sh).
 
     python scripts/traffic_run.py calib      # quiet engine: every launch moves exactly the group state
-    python scripts/traffic_run.py workload   # bench.py's config-3 workload, K=64 then K=1 launches
+    python scripts/traffic_run.py workload   # bench.py's config-3 workload, K=64, K=512, then K=1 launches
 
 The calibration engine never fires a timer, sends no message and appends
 nothing, so each step-kernel launch reads and writes exactly
@@ -29,9 +29,11 @@ def main(mode):
         e.step(20, counters=False)
     else:
         kw = dict(abi.CONFIGS[3], G=G)
-        e = RaftEngine(abi.make_params(log_cap=256, steps_per_launch=64, **kw))
+        e = RaftEngine(abi.make_params(log_cap=640, steps_per_launch=64, **kw))
         e.step(128, counters=False)        # warmup (2 launches)
         e.step(256, counters=False)        # 4 launches at K=64
+        e.set_steps_per_launch(512)
+        e.step(1024, counters=False)       # 2 launches at K=512 (bench default)
         e.set_steps_per_launch(1)
         e.step(20, counters=False)         # 20 launches at K=1
     e.close()

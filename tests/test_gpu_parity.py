@@ -152,15 +152,15 @@ def test_steps_per_launch_invariance():
     kw = dict(abi.CONFIGS[3])
     kw.update(G=5000, churn_ppm=10_000)
     digests = []
-    for k in (1, 7, 32, 128):
-        e = RaftEngine(abi.make_params(log_cap=300, steps_per_launch=k, **kw))
-        c = e.step(300)
+    for k in (1, 7, 32, 128, abi.MAX_STEPS_PER_LAUNCH):          # 600 = one full 512-step launch + 88
+        e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=k, **kw))
+        c = e.step(600)
         digests.append((e.digest(), c.tobytes()))
     # steps_per_launch changed mid-run (bench.py's streaming leg)
-    e = RaftEngine(abi.make_params(log_cap=300, steps_per_launch=64, **kw))
-    c1 = e.step(150)
+    e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=64, **kw))
+    c1 = e.step(300)
     e.set_steps_per_launch(1)
-    c2 = e.step(150)
+    c2 = e.step(300)
     digests.append((e.digest(), np.concatenate([c1, c2]).tobytes()))
     assert all(d == digests[0] for d in digests)
 
