@@ -39,6 +39,7 @@ constexpr int BLOCK = 256;
 __device__ unsigned long long g_phase_cycles[PH_N];   // diagnostic builds only
 #endif
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
+constexpr int JOB_LDS_WORDS = WAVES_PER_BLOCK * 64 * 4;   // step_kernel's per-wave job-word staging
 
 __device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
 
@@ -159,7 +160,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
     using L = Lanes<R>;
-    extern __shared__ uint32_t lds_cnt[];                                 // [nsteps][NCW]
+    // LDS: [WAVES_PER_BLOCK][64][4] the step's Philox job words (Ctx::jl),
+    // then the counter rows [nsteps][NCW]
+    extern __shared__ uint32_t lds[];
+    uint32_t* const lds_cnt = lds + JOB_LDS_WORDS;
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     const int wid = blockIdx.x * WAVES_PER_BLOCK + wib;
@@ -180,6 +184,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
     c.tw = c.dwt = c.dwv = 0u;
+    c.jl = lds + wib * 256;
 
     for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK) lds_cnt[q] = 0u;
     Node n;
@@ -549,7 +554,7 @@ template <int R> struct InitL {
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
-        const size_t lds = (size_t)k * NCW * 4;
+        const size_t lds = (size_t)(JOB_LDS_WORDS + k * NCW) * 4;
         if (e->p.mode == RAFT_MODE_TEXTBOOK)
             step_kernel<R, true><<<e->nblocks, BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
         else

@@ -408,6 +408,7 @@ struct Ctx {
     uint32_t part;            // replicas on side B of this step's partition
     uint2* lr;                // this replica's log
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
+    uint32_t* jl;             // the wave's LDS staging of the job words, [64 lanes][4]
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
@@ -451,12 +452,13 @@ __device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const C
     return word_of(w, q & 3);
 }
 
+// Word k of the job that lane job_lane of this lane's group drew, read from
+// the wave's LDS staging (one ds_read_b32 instead of four ds_bpermute and a
+// select).  Dead lanes may address past their wave's rows; their words are
+// never used.
 template <int R>
 __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int k) {
-    const int sl = c.src(job_lane);
-    const uint32_t a = bcastu(c.job.x, sl), b = bcastu(c.job.y, sl);
-    const uint32_t x = bcastu(c.job.z, sl), y = bcastu(c.job.w, sl);
-    return sel4(a, b, x, y, k);
+    return c.jl[(c.src(job_lane) << 2) + k];
 }
 
 template <int R, bool HAVE_JOB>
@@ -854,9 +856,15 @@ struct Stepper {
 #else
             c.job = draw(p, c.t, c.gid(), purpose, sub);
 #endif
-            hw0 = bcastu(c.job.x, c.base);
-            hw1 = bcastu(c.job.y, c.base);
-            hw2 = bcastu(c.job.z, c.base);
+            // stage the wave's jobs in LDS (one ds_write_b128 per lane); a
+            // wave's LDS accesses complete in order, so its reads below see
+            // them, and the previous step's reads were issued before this write
+            *(uint4*)&c.jl[(c.base + c.r) << 2] = make_uint4(c.job.x, c.job.y, c.job.z, c.job.w);
+            asm volatile("" ::: "memory");
+            const uint4 h = *(const uint4*)&c.jl[c.base << 2];
+            hw0 = h.x;
+            hw1 = h.y;
+            hw2 = h.z;
             // every word this lane needs from the jobs, fetched in one batch
             c.tw = job_word(c, L::J_TIMER + (r >> 2), r & 3);
             if constexpr (L::TICK_JOB) c.dwt = job_drop_word(c, L::J_TICK, c.s_tick);
