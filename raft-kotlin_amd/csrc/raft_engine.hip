@@ -224,6 +224,11 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         cnt.clear();
         Stepper<R, TB>::step(p, c, n, cnt);
         c.clk.mark(PH_TDRAW);
+#ifdef RAFT_EXP_NO_FLUSH
+#pragma unroll
+        for (int cw = 0; cw < NCW; ++cw) asm volatile("" :: "s"(cnt.s[cw]));   // timing experiment only
+        continue;
+#endif
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
         for (int cw = 0; cw < NCW; ++cw) v = (uint32_t)raft_writelane((int32_t)cnt.s[cw], cw, (int32_t)v);
@@ -263,15 +268,24 @@ __global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
 // half (c & 1) of partials[k][c >> 1][b]; grid (chunks, nsteps * NC), the
 // counters zeroed beforehand (int64 atomics: exact and order-independent).
 constexpr int REDUCE_CHUNK = 16 * BLOCK;
+// APPEND_SKIPPED is derived per workgroup partial as R * SESSIONS_TICKED -
+// APPEND_SENT (the step kernel does not count it, see Stepper::tick).
+__device__ __forceinline__ uint32_t half16(const uint32_t* part, int64_t k, int c, int64_t nparts, int b) {
+    return (part[(k * NCW + (c >> 1)) * nparts + b] >> (16 * (c & 1))) & 0xFFFFu;
+}
 __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* __restrict__ partials, int nparts,
-                                                                int64_t* __restrict__ counters) {
+                                                                int R, int64_t* __restrict__ counters) {
     __shared__ uint32_t acc[WAVES_PER_BLOCK];
     const int k = blockIdx.y / NC, c = blockIdx.y % NC;
-    const uint32_t* src = partials + ((int64_t)k * NCW + (c >> 1)) * nparts;
-    const int sh = 16 * (c & 1);
     const int b1 = min(nparts, (int)(blockIdx.x + 1) * REDUCE_CHUNK);
     uint32_t v = 0;                 // < 2^16 * 16 per thread
-    for (int b = blockIdx.x * REDUCE_CHUNK + threadIdx.x; b < b1; b += BLOCK) v += (src[b] >> sh) & 0xFFFFu;
+    if (c == RAFT_C_APPEND_SKIPPED) {
+        for (int b = blockIdx.x * REDUCE_CHUNK + threadIdx.x; b < b1; b += BLOCK)
+            v += (uint32_t)R * half16(partials, k, RAFT_C_SESSIONS_TICKED, nparts, b) -
+                 half16(partials, k, RAFT_C_APPEND_SENT, nparts, b);
+    } else {
+        for (int b = blockIdx.x * REDUCE_CHUNK + threadIdx.x; b < b1; b += BLOCK) v += half16(partials, k, c, nparts, b);
+    }
     const uint32_t ws = __ockl_wfred_add_u32(v);   // < 2^16 * REDUCE_CHUNK = 2^28
     if ((threadIdx.x & 63) == 0) acc[threadIdx.x >> 6] = ws;
     __syncthreads();
@@ -754,7 +768,7 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
         HIP_TRY(hipMemsetAsync(dst, 0, (size_t)k * RAFT_COUNTER_STRIDE * 8, e->stream));
         const dim3 rg((unsigned)((e->nblocks + REDUCE_CHUNK - 1) / REDUCE_CHUNK), (unsigned)(k * NC));
-        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, dst);
+        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, e->p.R, dst);
         done += k;
     }
     HIP_TRY(hipGetLastError());

@@ -596,7 +596,9 @@ struct Stepper {
         const uint64_t has = pge & lm(i <= Llast);
         cnt.add(run & p0 & plt, RAFT_C_PREV_READS_LEADER);
         cnt.add(run & has, RAFT_C_ENTRY_READS_LEADER);
-        cnt.add(run & ~ok, RAFT_C_APPEND_SKIPPED);
+        // RAFT_C_APPEND_SKIPPED (run & ~ok) is not counted here: run covers
+        // whole groups, so it is R * SESSIONS_TICKED - APPEND_SENT, which the
+        // counter reduction derives (reduce_counters_kernel)
         cnt.add(ok, RAFT_C_APPEND_SENT);
         // every log slot of the tick, resolved up front: the leader's log[prev]
         // and log[i-1], and this replica's own log[prev] (append() :274-276);
@@ -669,6 +671,7 @@ struct Stepper {
             // it (as 16 << q) to the popcount: pc >= (16 << q) + MAJ tests
             // "response q acked and count >= majority" in one compare
             const uint32_t ck16 = c.gbits(chk) << 4;
+            uint64_t commits = 0;                                         // one lane per increment
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 if (!(chk & L::lanes_of(q))) continue;                    // wave-uniform
@@ -677,8 +680,9 @@ struct Stepper {
                 const uint32_t pc = __popc(gt) + (ck16 & (16u << q));
                 const uint64_t inc = lm(pc >= (16u << q) + MAJ);          // :162 (whole groups)
                 C = inc_if(C, inc);
-                cnt.add(inc & L::lanes_of(q), RAFT_C_COMMITS);
+                commits |= inc & L::lanes_of(q);                          // disjoint lanes per q
             }
+            cnt.add(commits, RAFT_C_COMMITS);
         }
         if constexpr (TB) {
             // textbook commit rule: N = the majority-th largest matchIndex of the
