@@ -39,7 +39,14 @@ constexpr int BLOCK = 256;
 __device__ unsigned long long g_phase_cycles[PH_N];   // diagnostic builds only
 #endif
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
-constexpr int JOB_LDS_WORDS = WAVES_PER_BLOCK * 64 * 4;   // step_kernel's per-wave job-word staging
+// step_kernel's workgroup: its LDS holds one counter row per step for the
+// whole workgroup, so larger workgroups leave room for longer launches
+#ifndef RAFT_STEP_BLOCK
+#define RAFT_STEP_BLOCK 256
+#endif
+constexpr int STEP_BLOCK = RAFT_STEP_BLOCK;
+constexpr int STEP_WAVES = STEP_BLOCK / 64;
+constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
 
 __device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
 
@@ -156,17 +163,17 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 #define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
 #endif
 template <int R, bool TB>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
+__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
     using L = Lanes<R>;
-    // LDS: [WAVES_PER_BLOCK][64][4] the step's Philox job words (Ctx::jl),
+    // LDS: [STEP_WAVES][64][4] the step's Philox job words (Ctx::jl),
     // then the counter rows [nsteps][NCW]
     extern __shared__ uint32_t lds[];
     uint32_t* const lds_cnt = lds + JOB_LDS_WORDS;
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    const int wid = blockIdx.x * WAVES_PER_BLOCK + wib;
+    const int wid = blockIdx.x * STEP_WAVES + wib;
     const int j = lane / R;
     const int r = lane - j * R;
     const int64_t g = (int64_t)wid * L::GPW + j;
@@ -186,7 +193,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.tw = c.dwt = c.dwv = 0u;
     c.jl = lds + wib * 256;
 
-    for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK) lds_cnt[q] = 0u;
+    for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
     Node n;
     c.clk.start();
     if (live) load_node(n, p, g, idx);
@@ -232,12 +239,12 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
         for (int cw = 0; cw < NCW; ++cw) v = (uint32_t)raft_writelane((int32_t)cnt.s[cw], cw, (int32_t)v);
-        // < 2^16 per half per workgroup: a wave counts < 2^14 events of a kind per step
+        // < 2^16 per half per workgroup: a wave counts < 2^13 events of a kind per step
         if (lane < NCW) __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         c.clk.mark(PH_CNT);
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < nsteps * NCW; q += BLOCK)               // workgroup partials
+    for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK)               // workgroup partials
         partials[(int64_t)q * gridDim.x + blockIdx.x] = lds_cnt[q];
 #ifdef RAFT_PROFILE_PHASES
     if (lane == 0)
@@ -534,7 +541,7 @@ struct raft_engine {
     size_t bytes;
     uint64_t t;
     int K;                      // steps per launch
-    int nblocks;                // step-kernel workgroups: ceil(G / (WAVES_PER_BLOCK * (64 / R)))
+    int nblocks;                // step-kernel workgroups: ceil(G / (STEP_WAVES * (64 / R)))
     uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials
     int64_t* counters_dev;      // [K][STRIDE] scratch
     // step-kernel event timing
@@ -570,9 +577,9 @@ template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
         const size_t lds = (size_t)(JOB_LDS_WORDS + k * NCW) * 4;
         if (e->p.mode == RAFT_MODE_TEXTBOOK)
-            step_kernel<R, true><<<e->nblocks, BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
+            step_kernel<R, true><<<e->nblocks, STEP_BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
         else
-            step_kernel<R, false><<<e->nblocks, BLOCK, lds, e->stream>>>(e->dp, t0, k,
+            step_kernel<R, false><<<e->nblocks, STEP_BLOCK, lds, e->stream>>>(e->dp, t0, k,
                                                                                              e->partials);
     }
 };
@@ -671,7 +678,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.churn_thr32 = ppm_thr(p->churn_ppm, 32); d.cmd_thr32 = ppm_thr(p->cmd_ppm, 32);
     d.churn_steps = p->churn_steps; d.part_period = p->partition_period; d.part_len = p->partition_len;
     d.cmd_mode = p->cmd_mode; d.cmd_limit = p->cmd_limit;
-    const int64_t gpb = (int64_t)WAVES_PER_BLOCK * (64 / p->R);     // groups per step workgroup
+    const int64_t gpb = (int64_t)STEP_WAVES * (64 / p->R);          // groups per step workgroup
     e->nblocks = (int)((G + gpb - 1) / gpb);
     d.GR = G * R;
     e->K = p->steps_per_launch > 0 ? p->steps_per_launch : 1;
