@@ -161,9 +161,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a one-GPU box (never set by the driver):
+    # RAFT_BENCH_BACKEND=gloo with RAFT_BENCH_ONE_DEVICE=1 runs every rank on
+    # cuda:0 with gloo collectives, which exercises the N > 1 path end to end
+    backend = os.environ.get("RAFT_BENCH_BACKEND", "nccl")
+    if os.environ.get("RAFT_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     eng_mod = importlib.import_module("raft-kotlin_amd.engine")
