@@ -382,6 +382,8 @@ struct Lanes {
     static constexpr bool JOBS = 1 + NQ <= R;          // harness + timer quads fit
     static constexpr bool TICK_JOB = JOBS && J_TICK + NCH <= R;
     static constexpr bool VOTE_JOB = JOBS && J_VOTE + NCH <= R;
+    // one chunk per sender: a pass of the group's R lanes covers every sender
+    static constexpr bool VOTE_ALL = NCH == 1;
 
     // lanes whose replica index is s (compile-time masks)
     // lanes whose replica index is <= s
@@ -725,6 +727,7 @@ struct Stepper {
     // One RequestVote round: every group with a pending sender delivers the
     // requests of its lowest remaining sender s to all destinations at once.
     // Predicated, called in wave-uniform control flow.
+    template <bool STAGED = false>
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
                                                       uint32_t& vtodo, uint32_t send, int32_t qt, int32_t qli,
                                                       int32_t qlt) {
@@ -737,7 +740,9 @@ struct Stepper {
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
         const uint64_t mvr = lm(vr);
-        const uint32_t dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
+        uint32_t dw;
+        if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // sender s's chunk, row of lane s
+        else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t lreq = mine & lost(p, c, s, r, dw, 0);       // retry{} swallows, Commons.kt:41
         const uint64_t act = mine & ~lreq;
@@ -910,8 +915,24 @@ struct Stepper {
         uint32_t vtodo = c.gbits(__ballot(send != 0));
         if (__ballot(vtodo != 0)) {
             vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
-            while (__ballot(vtodo != 0))                                    // groups with 2+ senders (rare)
-                vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+            if (__ballot(vtodo != 0)) {                                     // groups with 2+ senders
+                if constexpr (L::VOTE_ALL) {
+                    // one Philox pass draws the drop-word chunk of EVERY sender of
+                    // the group (lane r: sender r, the chunk drop_word_direct
+                    // would draw), staged over the job rows (consumed by now):
+                    // the later rounds read their words from LDS, no pass each
+                    if (p.drop_thr16 != 0) {
+                        const u32x4 w = draw(p, c.t, c.gid(), RAFT_RNG_VOTE_DROP, (uint32_t)r);
+                        *(uint4*)&c.jl[(c.base + r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
+                        asm volatile("" ::: "memory");
+                    }
+                    do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                    while (__ballot(vtodo != 0));
+                } else {
+                    do vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                    while (__ballot(vtodo != 0));
+                }
+            }
         }
 
         c.clk.mark(PH_V);
