@@ -383,7 +383,7 @@ struct Lanes {
     static constexpr bool TICK_JOB = JOBS && J_TICK + NCH <= R;
     static constexpr bool VOTE_JOB = JOBS && J_VOTE + NCH <= R;
     // one chunk per sender: a pass of the group's R lanes covers every sender
-    static constexpr bool VOTE_ALL = NCH == 1;
+    static constexpr bool SENDERS_STAGED = NCH == 1;
 
     // lanes whose replica index is s (compile-time masks)
     // lanes whose replica index is <= s
@@ -566,6 +566,7 @@ struct Stepper {
     // are built from the leader's tick-start snapshot (S-4) and delivered to
     // all destinations at once; responses are replayed in destination order.
     // Predicated, called in wave-uniform control flow.
+    template <bool STAGED = false>
     __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, bool tk, int s,
                                                 Counters& cnt) {
         const int sl = c.src(s);
@@ -577,7 +578,9 @@ struct Stepper {
         const uint32_t Lc1 = bcastu(n.c1, sl);
         const uint64_t mtk = lm(tk), mme = lm(c.r == s);
         const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
-        const uint32_t dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
+        uint32_t dw;
+        if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
+        else dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
         n.fl &= ib(mtk & ~run & mme) ? ~FL_HB : ~0u;                      // :117 cancel() (S-10)
         cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
         const uint64_t swap = run & lm(n.s0 != s);                        // swap the session in (rare)
@@ -724,6 +727,19 @@ struct Stepper {
         n.fl |= (sd && !(n.fl & FL_ELECTING)) ? (FL_ARMED | FL_DRAW) : 0u;
     }
 
+    // The drop-word chunk of EVERY sender of the group in one Philox pass of
+    // the wave (lane r: sender r, the chunk drop_word_direct would draw),
+    // staged over the job rows, whose words are all fetched by now.  The
+    // second and later vote / tick rounds of a step read their words from LDS
+    // (job_drop_word(c, s, s)) instead of one direct pass each.  Called in
+    // wave-uniform control flow.
+    __device__ __forceinline__ static void stage_sender_chunks(const DevParams& p, Ctx<R>& c, uint32_t purpose) {
+        if (p.drop_thr16 == 0) return;
+        const u32x4 w = draw(p, c.t, c.gid(), purpose, (uint32_t)c.r);
+        *(uint4*)&c.jl[(c.base + c.r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
+        asm volatile("" ::: "memory");
+    }
+
     // One RequestVote round: every group with a pending sender delivers the
     // requests of its lowest remaining sender s to all destinations at once.
     // Predicated, called in wave-uniform control flow.
@@ -741,7 +757,7 @@ struct Stepper {
         const int32_t st = bcast(n.term, sl);
         const uint64_t mvr = lm(vr);
         uint32_t dw;
-        if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // sender s's chunk, row of lane s
+        if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t lreq = mine & lost(p, c, s, r, dw, 0);       // retry{} swallows, Commons.kt:41
@@ -916,16 +932,8 @@ struct Stepper {
         if (__ballot(vtodo != 0)) {
             vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
             if (__ballot(vtodo != 0)) {                                     // groups with 2+ senders
-                if constexpr (L::VOTE_ALL) {
-                    // one Philox pass draws the drop-word chunk of EVERY sender of
-                    // the group (lane r: sender r, the chunk drop_word_direct
-                    // would draw), staged over the job rows (consumed by now):
-                    // the later rounds read their words from LDS, no pass each
-                    if (p.drop_thr16 != 0) {
-                        const u32x4 w = draw(p, c.t, c.gid(), RAFT_RNG_VOTE_DROP, (uint32_t)r);
-                        *(uint4*)&c.jl[(c.base + r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
-                        asm volatile("" ::: "memory");
-                    }
+                if constexpr (L::SENDERS_STAGED) {
+                    stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
                     do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt);
                     while (__ballot(vtodo != 0));
                 } else {
@@ -974,11 +982,15 @@ struct Stepper {
                 todo &= todo - 1u;
                 tick(p, c, n, tk, s, cnt);
             }
-            while (__ballot(todo != 0)) {                                   // 2+ sessions (rare)
-                const bool tk = todo != 0;
-                const int s = tk ? __builtin_ctz(todo) : 0;
-                todo &= todo - 1u;
-                tick(p, c, n, tk, s, cnt);
+            if (__ballot(todo != 0)) {                                      // 2+ sessions (rare)
+                constexpr bool ALL = L::SENDERS_STAGED;
+                if constexpr (ALL) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
+                do {
+                    const bool tk = todo != 0;
+                    const int s = tk ? __builtin_ctz(todo) : 0;
+                    todo &= todo - 1u;
+                    tick<ALL>(p, c, n, tk, s, cnt);
+                } while (__ballot(todo != 0));
             }
         }
 
