@@ -929,7 +929,15 @@ struct Stepper {
         // runtime s), so the wave runs as many rounds as its busiest group has
         // senders -- usually one -- with one handler per destination lane.
         uint32_t vtodo = c.gbits(__ballot(send != 0));
-        if (__ballot(vtodo != 0)) {
+        if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
+            // the job lanes do not hold the first sender's chunk (R < 4): one
+            // staging pass serves every round, the first included
+            if (__ballot(vtodo != 0)) {
+                stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
+                do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                while (__ballot(vtodo != 0));
+            }
+        } else if (__ballot(vtodo != 0)) {
             vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
             if (__ballot(vtodo != 0)) {                                     // groups with 2+ senders
                 if constexpr (L::SENDERS_STAGED) {
@@ -977,14 +985,18 @@ struct Stepper {
         // the compiler carry the counters in VGPRs and copy the node per round)
         if (__ballot(todo != 0)) {
             {
+                // R = 2: the job lanes do not hold the first leader's chunk,
+                // so one staging pass serves every round, the first included
+                constexpr bool FIRST_STAGED = L::SENDERS_STAGED && !L::TICK_JOB;
+                if constexpr (FIRST_STAGED) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
                 const bool tk = todo != 0;
                 const int s = tk ? __builtin_ctz(todo) : 0;
                 todo &= todo - 1u;
-                tick(p, c, n, tk, s, cnt);
+                tick<FIRST_STAGED>(p, c, n, tk, s, cnt);
             }
             if (__ballot(todo != 0)) {                                      // 2+ sessions (rare)
                 constexpr bool ALL = L::SENDERS_STAGED;
-                if constexpr (ALL) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
+                if constexpr (ALL && L::TICK_JOB) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
                 do {
                     const bool tk = todo != 0;
                     const int s = tk ? __builtin_ctz(todo) : 0;
