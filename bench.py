@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py — Raft group-steps/sec of the MI355X batched Raft engine.
 
-Workload (BASELINE.json configs[2], "config 3"): 10^6 five-replica groups per
-GPU, seeded 5% message drop, leader-isolation churn (1e-3 per group-step, 15
+Workload (BASELINE.json configs[2], "config 3"): 10^6 five-replica groups,
+seeded 5% message drop, leader-isolation churn (1e-3 per group-step, 15
 steps), one client command per group-step with probability 1/4.  A "step" is
 one lockstep heartbeat period of every group: timers, the
 RequestVote phase, the AppendEntries/commit phase and client commands, with
@@ -11,10 +11,14 @@ all state resident in HBM before the timed region starts.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Multi-GPU: one process per GPU, each owns its own contiguous range of global
-group ids (weak scaling; no data-path collective).  The per-step global
-counters (commits, leaders, safety flags, ...) are all-reduced over RCCL in
-batches on a side stream.  Rank 0 prints ONE JSON line.
+Multi-GPU (BASELINE.json configs[3], "config 4"): one process per GPU.  With
+--gpus N > 1 and no torch.distributed environment, this script spawns the N
+rank processes itself (fresh interpreters; the parent makes no HIP or
+torch.cuda call) and exits with their status.  By default the 10^6 groups are
+split into contiguous global-id ranges (strong scaling); --scaling weak gives
+every GPU its own 10^6 groups.  Groups never talk across GPUs, so the only
+collective is the all-reduce of the per-step counter rows over RCCL, batched
+on a side stream.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -22,6 +26,8 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,10 +40,69 @@ abi = importlib.import_module("raft-kotlin_amd.abi")
 
 METRIC = "Raft group-steps/sec (whole node) at 1M×5-replica groups; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+# VALU issue peak: 1024 SIMDs (256 CUs x 4), a wave64 VALU instruction issues
+# over 2 cycles on a 32-lane SIMD (MI355X_MICROARCH.md), 2.4 GHz max clock
+SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2
+VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 # per replica: 10 canonical fields + the log-tail cache (t1, t2, c1) + the
 # primary-session column (nextIndex, matchIndex); per group: 3 harness words
 REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
 GROUP_BYTES = 4 * 3
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
+
+
+def shard(total: int, world: int, rank: int, scaling: str) -> tuple[int, int]:
+    """(first global group id, groups) of `rank`.  strong: `total` groups split
+    into contiguous ranges (the first total % world ranks take one more);
+    weak: every rank owns its own `total` groups."""
+    if scaling == "weak":
+        return rank * total, total
+    base, extra = divmod(total, world)
+    return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
+
+
+def launch_length(steps: int, spl: int) -> int:
+    """Steps per launch of the timed region: the largest divisor of `steps`
+    that is <= spl, so every timed launch has the same length (its roofline
+    and PMC row then describe every launch); spl itself when no divisor
+    within a factor 4 of it exists."""
+    for d in range(min(spl, steps), 0, -1):
+        if steps % d == 0:
+            return d if d * 4 >= min(spl, steps) else min(spl, steps)
+    return max(1, min(spl, steps))
+
+
+def launch_plan(n: int, k: int) -> list[int]:
+    """Launch lengths of raft_engine_step_async(n) at steps_per_launch k."""
+    out = []
+    while n > 0:
+        out.append(min(k, n))
+        n -= out[-1]
+    return out
+
+
+def available_cpus() -> int:
+    """CPUs this process may really use: its affinity set, capped by a cgroup
+    CPU quota (a GPU box's share of the host is a quota, while os.cpu_count()
+    shows every CPU of the machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def algorithmic_bytes(c: np.ndarray, G: int, R: int) -> float:
@@ -71,19 +136,87 @@ def state_crossing_bytes(c: np.ndarray, G: int, R: int, launches: int) -> float:
     return state + log
 
 
-def load_traffic(workload: dict):
-    """HBM traffic per launch measured by rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    for this exact workload (scripts/traffic.sh -> profiles/traffic.json), or None."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+def load_pmc(key: dict):
+    """The rocprofv3 PMC row (scripts/pmc_bench.sh -> profiles/pmc_rows.json)
+    of exactly this workload and launch length, or None: HBM bytes per launch
+    (FETCH_SIZE + WRITE_SIZE, separate passes, calibrated factors) and SQ
+    instruction counts per launch."""
     try:
-        with open(path) as f:
-            rows = json.load(f)
+        rows = json.load(open(PMC_FILE))
     except (OSError, ValueError):
         return None
     for row in rows:
-        if all(row.get(k) == v for k, v in workload.items()):
+        if all(row.get(k) == v for k, v in key.items()):
             return row
     return None
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """Run this script as n rank processes on this node (one per GPU) and
+    return their combined exit status.  Called before anything touches a GPU:
+    the children are fresh interpreters, never an exec of this process."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # only rank 0 writes the result line to stdout; the others' output goes to stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:                                   # one rank failed: the others would hang in a collective
+                rc = bad[0]
+                break
+            time.sleep(0.05)
+        rc = rc or next((p.returncode for p in procs if p.returncode not in (None, 0)), 0)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10_000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--groups", type=int, default=1_000_000,
+                    help="total groups (strong scaling) or groups per GPU (weak scaling)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
+                    help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
+    ap.add_argument("--steps-per-launch", type=int, default=512,
+                    help="upper bound of the lockstep steps fused into one kernel launch (state stays in VGPRs)")
+    ap.add_argument("--stream-steps", type=int, default=200,
+                    help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
+    ap.add_argument("--log-cap", type=int, default=0)
+    ap.add_argument("--reduce-every", type=int, default=512,
+                    help="steps per counter all-reduce (rounded to whole launches)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds-1t", type=float, default=5.0, help="target seconds of the single-thread CPU leg")
+    ap.add_argument("--cpu-chunk", type=int, default=20)
+    ap.add_argument("--plan-file", default="",
+                    help="write the step-kernel launch sequence (leg, steps) and the workload key as JSON, for "
+                         "attributing rocprofv3 dispatches (scripts/pmc_bench.sh)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="no GPU: start the ranks, agree on the shards over gloo, print them (tests)")
+    return ap.parse_args(argv)
 
 
 def cpu_baseline(args, kw, log_cap, total_steps):
@@ -94,7 +227,7 @@ def cpu_baseline(args, kw, log_cap, total_steps):
     calibrated so that the timed part takes about --cpu-seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = args.cpu_threads or available_cpus()
     # calibration: a short run of a small sample
     probe = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=args.cpu_groups)))
     t0 = time.perf_counter()
@@ -126,41 +259,47 @@ def cpu_baseline(args, kw, log_cap, total_steps):
                       f"({args.warmup} untimed), {dt:.1f} s, pthreads over groups",
             "single_thread": {"value": value1, "unit": "group-steps/s", "cores": 1,
                               "sample": f"global groups 0..{G1 - 1}, same steps, {dt1:.1f} s"},
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+
+
+def plan_only(args, world, rank):
+    """The rank/shard plumbing without a GPU (tests/test_bench_cpu.py)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    g0, n = shard(args.groups, world, rank, args.scaling)
+    t = torch.tensor([rank, g0, n], dtype=torch.int64)
+    rows = [torch.zeros_like(t) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(rows, t)
+    else:
+        rows = [t]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "scaling": args.scaling,
+                          "shards": [[int(x) for x in r.tolist()] for r in rows]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10_000)
-    ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--groups", type=int, default=1_000_000, help="groups per GPU")
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
-    ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
-                    help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
-    ap.add_argument("--steps-per-launch", type=int, default=512,
-                    help="lockstep steps fused into one kernel launch (state stays in VGPRs)")
-    ap.add_argument("--stream-steps", type=int, default=200,
-                    help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
-    ap.add_argument("--log-cap", type=int, default=0)
-    ap.add_argument("--reduce-every", type=int, default=512,
-                    help="steps per counter all-reduce (and per step_async call: keep it a multiple of --steps-per-launch)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-seconds-1t", type=float, default=5.0, help="target seconds of the single-thread CPU leg")
-    ap.add_argument("--cpu-chunk", type=int, default=20)
-    ap.add_argument("--warmup-cpu", type=int, default=40)
-    args = ap.parse_args()
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return spawn_ranks(args.gpus)                 # the parent never touches a GPU
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        return 2
+    if args.plan_only:
+        plan_only(args, world, rank)
+        return 0
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs for a one-GPU box (never set by the driver):
     # RAFT_BENCH_BACKEND=gloo with RAFT_BENCH_ONE_DEVICE=1 runs every rank on
     # cuda:0 with gloo collectives, which exercises the N > 1 path end to end
@@ -178,22 +317,21 @@ def main():
     eng_mod = importlib.import_module("raft-kotlin_amd.engine")
     kw = dict(abi.CONFIGS[args.config])
     R = kw["R"]
-    if args.scaling == "weak":
-        G_local = args.groups
-        g0 = rank * G_local
-    else:
-        G_local = args.groups // world + (1 if rank < args.groups % world else 0)
-        g0 = rank * (args.groups // world) + min(rank, args.groups % world)
+    g0, G_local = shard(args.groups, world, rank, args.scaling)
+    groups_per_rank = [shard(args.groups, world, q, args.scaling)[1] for q in range(world)]
+    total_groups = sum(groups_per_rank)
     total_steps = args.warmup + args.steps + args.stream_steps
     # physical slots a replica can fill: ~0.3 per step at config 3's command
     # rate, up to one per step where every leader takes a command each step
     log_cap = args.log_cap or int(64 + (1.0 if kw["cmd_ppm"] >= 1_000_000 else 0.3) * total_steps)
-    spl = args.steps_per_launch
+    L = launch_length(args.steps, args.steps_per_launch)   # every timed launch has L steps
+    chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
     mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
-    params = abi.make_params(log_cap=log_cap, steps_per_launch=spl, mode=mode, **dict(kw, G=G_local, g0=g0))
+    params = abi.make_params(log_cap=log_cap, steps_per_launch=L, mode=mode, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+    gcounters = torch.zeros_like(counters) if world > 1 else counters
     wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
 
     # ---- warmup (untimed) ----
@@ -216,16 +354,18 @@ def main():
     ev0.record(stream)
     done = 0
     while done < args.steps:
-        k = min(args.reduce_every, args.steps - done)
+        k = min(chunk, args.steps - done)
         eng.step_async(k, counters[done].data_ptr())
         if world > 1:
             # the only collective: the batched per-step counter all-reduce,
-            # off the critical path on a side stream (counters never feed back)
+            # off the critical path on a side stream (counters never feed
+            # back); this rank's own rows stay in `counters`
             ev = torch.cuda.Event()
             ev.record(stream)
             comm_stream.wait_event(ev)
             with torch.cuda.stream(comm_stream):
-                dist.all_reduce(counters[done:done + k])
+                gcounters[done:done + k].copy_(counters[done:done + k])
+                dist.all_reduce(gcounters[done:done + k])
         done += k
     ev1.record(stream)
     eng.sync()
@@ -238,36 +378,54 @@ def main():
     eng.set_kernel_timing(False)
 
     elapsed = max(wall, ev_ms / 1e3)
+    kern_avg_ms = kern_ms / max(1, launches)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        ka = torch.tensor([kern_avg_ms], dtype=torch.float64, device=dev)
+        kall = [torch.zeros_like(ka) for _ in range(world)]
+        dist.all_gather(kall, ka)
+        kern_avg_per_rank = [float(x.item()) for x in kall]
+    else:
+        kern_avg_per_rank = [kern_avg_ms]
 
-    c_all = counters.cpu().numpy()[:, : abi.NUM_COUNTERS]     # already global if world > 1
-    local_counts = None
-    if world == 1:
-        local_counts = c_all
-    total_groups = G_local * world if args.scaling == "weak" else args.groups
+    c_all = gcounters.cpu().numpy()[:, : abi.NUM_COUNTERS]    # all ranks' groups
+    c_loc = counters.cpu().numpy()[:, : abi.NUM_COUNTERS]     # this rank's groups (before the all-reduce)
     value = total_groups * args.steps / elapsed
 
-    # roofline of the dominant kernel (step_kernel), from this rank's counters
-    if world > 1:
-        # the all-reduced counters are global; scale to this rank's share
-        local_counts = c_all * (G_local / total_groups)
-    kern_avg_ms = kern_ms / max(1, launches)
+    # roofline of the dominant kernel (step_kernel), from this rank's own counters
+    timed_plan = [x for q in range(0, args.steps, chunk) for x in launch_plan(min(chunk, args.steps - q), L)]
     kern_s = kern_ms / 1e3
-    bytes_alg = algorithmic_bytes(local_counts, G_local, R)
-    bytes_state = state_crossing_bytes(local_counts, G_local, R, launches)
+    bytes_alg = algorithmic_bytes(c_loc, G_local, R)
+    bytes_state = state_crossing_bytes(c_loc, G_local, R, launches)
     achieved = bytes_alg / kern_s / 1e9 if launches else 0.0
     achieved_state = bytes_state / kern_s / 1e9 if launches else 0.0
     overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
-    K = spl or 1
-    tr = load_traffic({"config": args.config, "groups": G_local, "steps_per_launch": K})
+    pmc_key = {"config": args.config, "mode": args.mode, "groups": G_local, "launch_steps": L,
+               "warmup": args.warmup, "steps": args.steps}
+    pmc = load_pmc(dict(pmc_key, leg="timed")) if len(set(timed_plan)) == 1 else None
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    roofline_valu = None
+    if pmc and pmc.get("valu_per_launch"):
+        ips = pmc["valu_per_launch"] / (kern_avg_ms / 1e3) / 1e9
+        roofline_valu = {
+            "bound": "valu", "achieved": ips, "peak": VALU_PEAK_GIPS, "unit": "G wave-instructions/s",
+            "frac": ips / VALU_PEAK_GIPS,
+            "valu_per_wave_step": pmc["valu_per_launch"] / (pmc["waves"] * L),
+            "salu_per_wave_step": pmc["salu_per_launch"] / (pmc["waves"] * L),
+            "valu_per_simd_cycle": pmc["valu_per_launch"] / (SIMDS * CLOCK_HZ * kern_avg_ms / 1e3),
+            "source": pmc["source"],
+            "note": "SQ_INSTS_VALU of this exact launch (rocprofv3 --pmc, same workload and launch length) / the "
+                    "live average launch time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU "
+                    "instruction (MI355X_MICROARCH.md). The fused kernel is VALU-issue bound: this is its "
+                    "binding roofline",
+        }
 
     # ---- streaming leg (untimed for `value`): one step per launch, so every
     # launch streams the whole group state HBM -> VGPRs -> HBM.  Its roofline
     # is the HBM-bound formulation of the same step. ----
-    stream = None
+    streaming = None
     if args.stream_steps > 0:
         eng.set_steps_per_launch(1)
         sc = torch.zeros((args.stream_steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
@@ -281,14 +439,23 @@ def main():
         s_bytes = algorithmic_bytes(cs, G_local, R) / max(1, s_n)
         s_state = state_crossing_bytes(cs, G_local, R, s_n) / max(1, s_n)
         s_ach = s_bytes / (s_avg / 1e3) / 1e9
-        s_tr = load_traffic({"config": args.config, "groups": G_local, "steps_per_launch": 1})
-        stream = {"steps_per_launch": 1, "steps": args.stream_steps, "kernel_avg_ms": s_avg,
-                  "alg_bytes_per_launch": s_bytes, "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                  "frac": s_ach / HBM_PEAK_GBS, "traffic": s_tr["bytes_per_launch"] if s_tr else None,
-                  "state_bytes_per_launch": s_state,
-                  "achieved_state_crossing": s_state / (s_avg / 1e3) / 1e9,
-                  "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
-                  "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
+        s_pmc = load_pmc(dict(pmc_key, launch_steps=1, leg="streaming", stream_steps=args.stream_steps))
+        streaming = {"steps_per_launch": 1, "steps": args.stream_steps, "kernel_avg_ms": s_avg,
+                     "alg_bytes_per_launch": s_bytes, "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": s_ach / HBM_PEAK_GBS,
+                     "traffic": s_pmc["hbm_bytes_per_launch"] if s_pmc else None,
+                     "traffic_frac": (s_pmc["hbm_bytes_per_launch"] / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS
+                                      if s_pmc else None),
+                     "state_bytes_per_launch": s_state,
+                     "achieved_state_crossing": s_state / (s_avg / 1e3) / 1e9,
+                     "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
+                     "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
+
+    if args.plan_file and rank == 0:
+        seq = [["warmup", x] for x in launch_plan(args.warmup, L)] + [["timed", x] for x in timed_plan]
+        seq += [["streaming", 1]] * args.stream_steps
+        json.dump({"key": pmc_key, "stream_steps": args.stream_steps, "R": R, "launches": seq},
+                  open(args.plan_file, "w"))
 
     # ---- safety flags (untimed): the run's counter-borne flags plus the
     # Log Matching check over committed prefixes ----
@@ -306,6 +473,7 @@ def main():
                 "properties); over the timed steps, Log Matching at the end of the run",
     }
 
+    cfg_name = "config4" if world > 1 and args.config == 3 and args.scaling == "strong" else f"config{args.config}"
     out = {
         "metric": METRIC,
         "value": value,
@@ -320,33 +488,37 @@ def main():
         "dtype": "int32",
         "data": "synthetic (seeded Philox harness: drops, churn, commands)",
         "config": {
-            "workload": f"config{args.config}: {G_local} groups/GPU x {R} replicas"
+            "workload": f"{cfg_name}: {total_groups} groups x {R} replicas"
+                        + (f" sharded by contiguous group id over {world} GPUs" if world > 1 else "")
                         + {3: ", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step",
                            5: ", 2-way partitions 25 of every 50 steps, 1 command per step to every leader",
                            2: ", no faults, 1/4 command per group-step"}[args.config]
                         + (", textbook mode" if mode else ""),
-            "groups_total": total_groups, "replicas": R, "log_cap": log_cap,
-            "steps_per_launch": K, "parallelism": f"shard-by-group x{world}",
-            "counter_allreduce_every": args.reduce_every if world > 1 else None,
+            "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
+            "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
+            "counter_allreduce_every": chunk if world > 1 else None,
         },
         "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
-            "kernel": f"step_kernel<{R}> x{K} fused steps", "kernel_avg_ms": kern_avg_ms, "launches": launches,
+            "bound": "hbm", "basis": "alg_equiv", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_frac": traffic / (kern_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "kernel": f"step_kernel<{R}> x{L} fused steps", "launch_steps": L,
+            "kernel_avg_ms": kern_avg_ms, "kernel_avg_ms_per_rank": kern_avg_per_rank, "launches": launches,
             "alg_bytes_per_launch": bytes_alg / max(1, launches),
-            "alg_bytes_per_group_step": bytes_alg / max(1, G_local * local_counts.shape[0]),
-            "traffic_source": tr["source"] if tr else None,
+            "alg_bytes_per_group_step": bytes_alg / max(1, G_local * c_loc.shape[0]),
+            "pmc_source": pmc["source"] if pmc else None,
             "state_bytes_per_launch": bytes_state / max(1, launches),
             "achieved_state_crossing": achieved_state,
             "frac_state_crossing": achieved_state / HBM_PEAK_GBS,
-            "note": "achieved = SURVEY.md §8(d) algorithmic bytes per group-step (event counts from the "
-                    "kernel's counters) x the group-steps of one launch / the launch's average duration. "
-                    "A fused launch keeps every replica in VGPRs for its K steps, so the HBM bytes it really "
-                    "moves (traffic, PMC) are far below the algorithmic bytes and the kernel is "
-                    "VALU-issue bound; achieved_state_crossing prices only the state a launch must move. "
-                    "roofline_streaming is the same step at one step per launch",
+            "note": "alg_equiv: achieved = SURVEY.md §8(d) algorithmic bytes per group-step (event counts from "
+                    "this rank's own kernel counters) x the group-steps of one launch / the launch's live average "
+                    "duration. A fused launch keeps every replica in VGPRs for its steps, so the HBM bytes it "
+                    "really moves (traffic, PMC of this exact launch, null if none was recorded) are far below "
+                    "the algorithmic bytes: traffic_frac is the measured HBM fraction, and roofline_valu is the "
+                    "binding roofline. roofline_streaming is the same step at one step per launch",
         },
-        "roofline_streaming": stream,
+        "roofline_valu": roofline_valu,
+        "roofline_streaming": streaming,
         "valid": overflow == 0,
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
@@ -358,7 +530,8 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

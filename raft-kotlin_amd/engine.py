@@ -131,6 +131,9 @@ class RaftEngine:
     def write_log(self, terms: np.ndarray, cmds: np.ndarray, g0: int = 0):
         t = np.ascontiguousarray(terms, dtype=np.int32)
         c = np.ascontiguousarray(cmds, dtype=np.uint32)
+        # the C side reads n * R * log_cap words from both arrays
+        if t.ndim != 3 or t.shape[1:] != (self.R, self.cap) or c.shape != t.shape:
+            raise ValueError(f"write_log: terms {t.shape} and cmds {c.shape} must both be (n, {self.R}, {self.cap})")
         self._check(self._lib.raft_engine_write_log(self._h, g0, t.shape[0], abi.ptr(t, C.c_int32),
                                                     abi.ptr(c, C.c_uint32)), "write_log")
 
@@ -151,12 +154,21 @@ class RaftEngine:
         return (int(out.value), f) if flags else int(out.value)
 
     # -- the service boundary (RaftServer.kt:228-287, :100-107) -------------
+    @staticmethod
+    def _batch_index(group, dst, n: int, what: str):
+        """group / dst as contiguous int64 / int32 vectors of exactly n entries
+        (the C side reads n of each)."""
+        g = np.ascontiguousarray(group, dtype=np.int64)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        if g.ndim != 1 or d.ndim != 1 or g.shape[0] != n or d.shape[0] != n:
+            raise ValueError(f"{what}: group {g.shape} and replica {d.shape} must be 1-D with {n} entries")
+        return g, d
+
     def vote_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
         """req: [n, 4] int32 (term, candidateId, lastLogIndex, lastLogTerm) ->
         [n, 2] int32 (term, voteGranted)."""
-        g = np.ascontiguousarray(group, dtype=np.int64)
-        d = np.ascontiguousarray(dst, dtype=np.int32)
         q = np.ascontiguousarray(req, dtype=np.int32).reshape(-1, 4)
+        g, d = self._batch_index(group, dst, q.shape[0], "vote_batch")
         out = np.zeros((q.shape[0], 2), dtype=np.int32)
         self._check(self._lib.raft_vote_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
                                               abi.ptr(q, abi.raft_vote_req), abi.ptr(out, abi.raft_vote_resp),
@@ -166,9 +178,8 @@ class RaftEngine:
     def append_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
         """req: [n, 8] int32 (term, leaderId, prevLogIndex, prevLogTerm, hasEntry,
         entryTerm, entryCmd(u32 bits), leaderCommit) -> [n, 3] (term, success, status)."""
-        g = np.ascontiguousarray(group, dtype=np.int64)
-        d = np.ascontiguousarray(dst, dtype=np.int32)
         q = np.ascontiguousarray(req).astype(np.int64).astype(np.uint32).view(np.int32).reshape(-1, 8)
+        g, d = self._batch_index(group, dst, q.shape[0], "append_batch")
         out = np.zeros((q.shape[0], 3), dtype=np.int32)
         self._check(self._lib.raft_append_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
                                                 abi.ptr(q, abi.raft_append_req), abi.ptr(out, abi.raft_append_resp),
@@ -176,9 +187,10 @@ class RaftEngine:
         return out
 
     def append_command_batch(self, group, replica, cmd):
-        g = np.ascontiguousarray(group, dtype=np.int64)
-        r = np.ascontiguousarray(replica, dtype=np.int32)
         c = np.ascontiguousarray(cmd, dtype=np.uint32)
+        if c.ndim != 1:
+            raise ValueError(f"append_command_batch: cmd {c.shape} must be 1-D")
+        g, r = self._batch_index(group, replica, c.shape[0], "append_command_batch")
         self._check(self._lib.raft_append_command_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(r, C.c_int32),
                                                         abi.ptr(c, C.c_uint32), c.shape[0]),
                     "raft_append_command_batch")

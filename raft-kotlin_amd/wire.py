@@ -21,6 +21,14 @@ def _check(rc: int, what: str) -> int:
     return rc
 
 
+# Upper bound of one encoded message without its command bytes: every int32
+# field is a 1-byte tag plus at most 10 varint bytes (negative values), i.e.
+# 11 B; RequestAppendEntriesRPC has 5 of them (55 B) plus entries[0]: a tag,
+# a <= 5-byte length, the entry's term (11 B), the command's tag and <= 5-byte
+# length (78 B before the command).  The other messages are smaller.
+MAX_FIXED_BYTES = 96
+
+
 def _pack(msgs: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
     off = np.zeros(len(msgs) + 1, dtype=np.int64)
     off[1:] = np.cumsum([len(m) for m in msgs])
@@ -44,7 +52,7 @@ def _encode(fn: str, arr: np.ndarray, width: int, ctype, extra=()) -> List[bytes
     a = np.ascontiguousarray(arr, dtype=np.int32).reshape(-1, width)
     n = a.shape[0]
     off = np.zeros(n + 1, dtype=np.int64)
-    cap = 64 * n + 64 + sum(int(x.nbytes) for x in extra if isinstance(x, np.ndarray))
+    cap = MAX_FIXED_BYTES * n + 16 + sum(int(x.nbytes) for x in extra if isinstance(x, np.ndarray))
     buf = np.zeros(cap, dtype=np.uint8)
     used = _check(getattr(_lib(), fn)(abi.ptr(a, ctype), *extra_args(extra), n, abi.ptr(buf, C.c_uint8), cap,
                                       abi.ptr(off, C.c_int64)), fn)

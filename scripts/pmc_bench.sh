@@ -1,0 +1,36 @@
+#!/bin/bash
+# rocprofv3 evidence for ONE bench.py command line (the exact command whose
+# JSON the numbers are attached to):
+#   1. a --kernel-trace --stats run (per-kernel average durations);
+#   2. PMC passes, one counter group per run and never combined with tracing:
+#      FETCH_SIZE | WRITE_SIZE | SQ instruction counts + GRBM_GUI_ACTIVE;
+#   3. the calibration engine (scripts/traffic_run.py calib) under FETCH_SIZE
+#      and WRITE_SIZE, whose launches move a known byte count;
+#   4. scripts/pmc_parse.py: per-launch rows keyed by the workload and launch
+#      length in $OUT/rows.json; back here, `python scripts/pmc_parse.py
+#      --merge gpurun_out/pmc_*/rows.json` folds them into
+#      profiles/pmc_rows.json (read by bench.py).
+#   TAG=r2_d20 ARGS="--steps 20 --warmup 5" scripts/pmc_bench.sh
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc_${TAG:-x}
+mkdir -p "$OUT"
+A="${ARGS:-} --no-cpu-baseline --plan-file $OUT/plan.json"
+echo "trace" >> "$OUT/status.txt"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
+    python bench.py $A > "$OUT/trace.log" 2>&1 || exit $?
+i=0
+for pmc in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  echo "pmc$i $pmc" >> "$OUT/status.txt"
+  timeout -s KILL 300 rocprofv3 --pmc $pmc -d "$OUT/pmc$i" -o run --output-format csv -- \
+      python bench.py $A > "$OUT/pmc$i.log" 2>&1 || exit $?
+done
+for c in FETCH_SIZE WRITE_SIZE; do
+  echo "calib $c" >> "$OUT/status.txt"
+  timeout -s KILL 120 rocprofv3 --pmc $c -d "$OUT/calib_$c" -o run --output-format csv -- \
+      python scripts/traffic_run.py calib > "$OUT/calib_$c.log" 2>&1 || exit $?
+done
+python scripts/pmc_parse.py "$OUT" && echo "parsed" >> "$OUT/status.txt"

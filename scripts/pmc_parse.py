@@ -1,0 +1,106 @@
+"""Parse scripts/pmc_bench.sh output into per-launch PMC rows of the step
+kernel, written to <dir>/rows.json; `--merge` folds such files into
+profiles/pmc_rows.json (bench.py attaches a row only to a run with the same
+workload key and launch length).
+
+Every step_kernel dispatch of a PMC pass is matched, in dispatch order, to
+the launch sequence bench.py wrote (--plan-file: warmup, timed and streaming
+launches with their step counts).  FETCH_SIZE / WRITE_SIZE are kilobytes per
+dispatch; the calibration engine, whose launches move exactly
+G * (R * 60 + 12) bytes, converts them to bytes for this kernel's 4-byte
+per-lane access pattern (MI355X_MICROARCH.md calibrates gfx950's factor for
+16 B/lane streams only)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
+CALIB_G, CALIB_R = int(os.environ.get("TRAFFIC_GROUPS", "1000000")), 5
+REPLICA_BYTES, GROUP_BYTES = 4 * 13 + 8, 12
+ID_FIELDS = ("config", "mode", "groups", "warmup", "steps", "leg", "launch_steps", "stream_steps")
+
+
+def dispatches(d):
+    """{counter: [value per step_kernel dispatch, in dispatch order]}; rows of
+    one dispatch (per-XCD or per-SE instances) are summed."""
+    acc = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            if "step_kernel" in row["Kernel_Name"]:
+                acc[row["Counter_Name"]][int(row["Dispatch_Id"])] += float(row["Counter_Value"])
+    return {c: [v for _, v in sorted(x.items())] for c, x in acc.items()}
+
+
+def mean(xs):
+    return sum(xs) / len(xs) if xs else None
+
+
+def main(d):
+    plan = json.load(open(os.path.join(d, "plan.json")))
+    seq = plan["launches"]
+    state = CALIB_G * (CALIB_R * REPLICA_BYTES + GROUP_BYTES)
+    cf = sorted(dispatches(f"{d}/calib_FETCH_SIZE").get("FETCH_SIZE", []))
+    cw = sorted(dispatches(f"{d}/calib_WRITE_SIZE").get("WRITE_SIZE", []))
+    ff = state / (cf[len(cf) // 2] * 1024.0)
+    wf = state / (cw[len(cw) // 2] * 1024.0)
+    per = {}
+    for p in sorted(glob.glob(f"{d}/pmc*")):
+        for c, vals in dispatches(p).items():
+            if len(vals) != len(seq):
+                raise SystemExit(f"{p}: {len(vals)} step_kernel dispatches, plan has {len(seq)}")
+            per[c] = vals
+    rows = []
+    for leg in ("timed", "streaming"):
+        ix = [i for i, (lg, _) in enumerate(seq) if lg == leg]
+        if not ix:
+            continue
+        steps = {seq[i][1] for i in ix}
+        if len(steps) != 1:
+            continue                                   # mixed launch lengths: no per-launch row
+        m = {c: mean([v[i] for i in ix]) for c, v in per.items()}
+        key = dict(plan["key"], leg=leg, launch_steps=steps.pop())
+        if leg == "streaming":
+            key["stream_steps"] = plan["stream_steps"]
+        row = dict(key)
+        row.update({
+            "hbm_bytes_per_launch": m["FETCH_SIZE"] * 1024.0 * ff + m["WRITE_SIZE"] * 1024.0 * wf,
+            "fetch_bytes_per_launch": m["FETCH_SIZE"] * 1024.0 * ff,
+            "write_bytes_per_launch": m["WRITE_SIZE"] * 1024.0 * wf,
+            "fetch_kb_raw": m["FETCH_SIZE"], "write_kb_raw": m["WRITE_SIZE"],
+            "fetch_factor": ff, "write_factor": wf, "calib_state_bytes": state,
+            "valu_per_launch": m.get("SQ_INSTS_VALU"), "salu_per_launch": m.get("SQ_INSTS_SALU"),
+            "lds_per_launch": m.get("SQ_INSTS_LDS"), "smem_per_launch": m.get("SQ_INSTS_SMEM"),
+            "waves": m.get("SQ_WAVES"), "wave_cycles": m.get("SQ_WAVE_CYCLES"),
+            "busy_cycles": m.get("SQ_BUSY_CYCLES"), "active_inst_valu": m.get("SQ_ACTIVE_INST_VALU"),
+            "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"), "launches_averaged": len(ix),
+            "source": f"rocprofv3 --pmc, separate passes (scripts/pmc_bench.sh, {os.path.basename(d)})",
+        })
+        rows.append(row)
+    json.dump(rows, open(os.path.join(d, "rows.json"), "w"), indent=1)
+    print(json.dumps(rows, indent=1))
+
+
+def merge(files):
+    """Merge parsed rows (gpurun_out/pmc_*/rows.json, pulled back from the GPU
+    box) into profiles/pmc_rows.json; a new row replaces one with the same key."""
+    try:
+        rows = json.load(open(OUT_FILE))
+    except (OSError, ValueError):
+        rows = []
+    ident = lambda r: tuple(r.get(k) for k in ID_FIELDS)  # noqa: E731
+    for f in files:
+        new = json.load(open(f))
+        keys = {ident(r) for r in new}
+        rows = [r for r in rows if ident(r) not in keys] + new
+    json.dump(rows, open(OUT_FILE, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--merge":
+        merge(sys.argv[2:])
+    else:
+        main(sys.argv[1])

@@ -76,3 +76,38 @@ def test_create_without_gpu_fails_loudly(lib):
     eng = importlib.import_module("raft-kotlin_amd.engine")
     with pytest.raises(eng.RaftError):
         eng.RaftEngine(abi.make_params(G=4))
+
+
+def _unbound_engine(R=5, cap=8):
+    """A RaftEngine shell without a device handle: the argument checks of the
+    batch wrappers run before any library call."""
+    eng = importlib.import_module("raft-kotlin_amd.engine")
+    e = object.__new__(eng.RaftEngine)
+    e.R, e.cap, e.G, e._h = R, cap, 4, None
+    return e
+
+
+@pytest.mark.parametrize("call", ["vote", "append", "command"])
+def test_batch_wrappers_reject_mismatched_lengths(call):
+    """group / replica / request arrays of different lengths would make the C
+    side read past the shorter host buffer: the wrapper refuses."""
+    e = _unbound_engine()
+    g3, d2, d3 = [0, 1, 2], [0, 1], [0, 1, 2]
+    with pytest.raises(ValueError):
+        if call == "vote":
+            e.vote_batch(g3, d2, [[1, 1, 0, 0]] * 3)
+        elif call == "append":
+            e.append_batch(g3, d3, [[1, 1, -1, -1, 0, 0, 0, 0]] * 2)
+        else:
+            e.append_command_batch(g3, d3, [7, 8])
+    with pytest.raises(ValueError):
+        e.vote_batch([[0, 1, 2]], d3, [[1, 1, 0, 0]] * 3)          # 2-D group index
+
+
+def test_write_log_rejects_wrong_shapes():
+    import numpy as np
+    e = _unbound_engine(R=3, cap=8)
+    with pytest.raises(ValueError):
+        e.write_log(np.zeros((2, 3, 8), np.int32), np.zeros((2, 3, 4), np.uint32))
+    with pytest.raises(ValueError):
+        e.write_log(np.zeros((2, 2, 8), np.int32), np.zeros((2, 2, 8), np.uint32))

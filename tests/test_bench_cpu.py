@@ -1,0 +1,68 @@
+"""bench.py's multi-GPU plumbing on CPU: `--gpus N` spawns N rank processes
+itself (no torch.distributed launcher), the ranks agree on their shards over
+gloo, a WORLD_SIZE that disagrees with --gpus is refused, and the shard
+arithmetic covers the global group ids exactly once (config 4: 10^6 groups
+split by contiguous global id)."""
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+spec = importlib.util.spec_from_file_location("bench", BENCH)
+bench = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(bench)
+
+
+def run(args, **env):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env)
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, env=e, timeout=240)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("total", [1_000_000, 999_999, 7])
+def test_strong_shards_cover_every_group_once(world, total):
+    spans = [bench.shard(total, world, r, "strong") for r in range(world)]
+    assert sum(n for _, n in spans) == total
+    nxt = 0
+    for g0, n in spans:
+        assert g0 == nxt and n >= total // world
+        nxt = g0 + n
+
+
+def test_weak_shards_are_disjoint_full_size():
+    spans = [bench.shard(1000, 4, r, "weak") for r in range(4)]
+    assert spans == [(0, 1000), (1000, 1000), (2000, 1000), (3000, 1000)]
+
+
+@pytest.mark.parametrize("steps,spl,want", [(10_000, 512, 500), (20, 512, 20), (1024, 512, 512), (7919, 512, 512),
+                                             (600, 512, 300), (5, 512, 5)])
+def test_timed_launches_have_one_length(steps, spl, want):
+    L = bench.launch_length(steps, spl)
+    assert L == want
+    if steps % L == 0:
+        assert set(bench.launch_plan(steps, L)) == {L}
+
+
+def test_gpus_2_spawns_two_gloo_ranks():
+    r = run(["--gpus", "2", "--plan-only"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout                      # rank 0 prints the one line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert out["shards"] == [[0, 0, 500_000], [1, 500_000, 500_000]]
+
+
+def test_world_size_mismatch_is_refused():
+    r = run(["--gpus", "4", "--plan-only"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_cpu_share_is_positive():
+    assert 1 <= bench.available_cpus() <= (os.cpu_count() or 1)

@@ -141,8 +141,10 @@ def test_config5_partitions_reduced():
     check_log_matching(e, o, "config5")
 
 
-@pytest.mark.parametrize("R", [1, 2, 3, 4, 6, 8])
+@pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_other_replica_counts(R):
+    """Drops, churn and partitions at every R: pins every staged and unstaged
+    drop-word chunk layout of the reference kernel (R = 5, 7 included)."""
     e, o = pair(R=R, G=3000, seed=100 + R, log_cap=300, drop_ppm=100_000, churn_ppm=20_000, churn_steps=15,
                 cmd_ppm=500_000, partition_period=40, partition_len=10)
     run_lockstep(e, o, 400, 50, f"R={R}")
@@ -218,7 +220,7 @@ def test_textbook_lockstep(cfg):
     assert check_log_matching(e, o, f"textbook config{cfg}") == 0
 
 
-@pytest.mark.parametrize("R", [1, 2, 4, 7, 8])
+@pytest.mark.parametrize("R", [1, 2, 3, 4, 5, 7, 8])
 def test_textbook_other_replica_counts(R):
     e, o = pair(R=R, G=2000, seed=200 + R, log_cap=300, drop_ppm=100_000, churn_ppm=20_000, churn_steps=15,
                 cmd_ppm=500_000, partition_period=40, partition_len=10, mode=abi.MODE_TEXTBOOK)
@@ -229,19 +231,22 @@ def test_textbook_other_replica_counts(R):
 FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_size.json")
 
 
+@pytest.mark.parametrize("spl", [1, abi.MAX_STEPS_PER_LAUNCH])
 @pytest.mark.parametrize("cfg", [3, 5])
-def test_full_size_digest(cfg):
+def test_full_size_digest(cfg, spl):
     """The north star's full-size runs, bit-exact: config 3 (10^6 x 5, 10^4
     steps) and config 5 (10^5 x 7, 10^4 steps) on the GPU against the oracle's
     whole-run digest (state, sessions and every physical log slot of every
     group) and its per-step counters, precomputed on the CPU by
-    tests/golden/make_full_size.py."""
+    tests/golden/make_full_size.py.  Run both one step per launch and with the
+    bench's fused 512-step launches (the exact kernel configuration bench.py
+    times)."""
     import json
     meta = json.load(open(FULL))[f"c{cfg}"]
     want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))[f"c{cfg}_counters"]
     kw = dict(abi.CONFIGS[cfg])
     assert meta["groups"] == kw["G"] and meta["params"] == {k: v for k, v in kw.items() if k != "G"}
-    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], **kw))
+    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], steps_per_launch=spl, **kw))
     ce = e.step(meta["steps"])
     if not np.array_equal(ce, want):
         bad = np.argwhere(ce != want)[0]
@@ -403,3 +408,59 @@ def test_session_started_and_deposed_in_one_step():
     s = o.read_state()[0]
     assert session(s, 3, 2)[0] == [1, 1, 1] and not (fld(s, 3, 2, "flags") & abi.FL_HB_ACTIVE)
     assert_same_state(e.read_state(), o.read_state(), 3, "group 53 step 13")
+
+
+def test_node_entries_term_command_dump():
+    """RaftServer.entries() (RaftServer.kt:96-97, served at :84-86): the
+    visible log log[0 .. lastIndex) (Commons.kt:71-72) as "term: command"
+    strings.  K7's trace through RaftService: after appendCommand("d") the
+    leader's physical log is [a, b, c, d] but its visible entries are [a, b]
+    (ghost tail, Q1), so tick 3 ships the stale `b` and every node shows
+    ["1: a", "1: b"].  Then a config-2 run: every node's dump equals the one
+    formatted from the oracle's log."""
+    service_mod = importlib.import_module("raft-kotlin_amd.service")
+    R = 3
+    e = RaftEngine(abi.make_params(R=R, G=1, log_cap=64))
+    svc = service_mod.RaftService(e)
+    ids = [svc.commands.intern(x) for x in "abc"]
+    w = blank_groups(1, R)
+    for r in range(R):
+        set_fld(w, R, r, "term", 1)
+        set_fld(w, R, r, "voted", 1)
+        if r:
+            set_fld(w, R, r, "flags", abi.FL_ARMED)
+            set_fld(w, R, r, "election_ms", 10 ** 9)
+    set_fld(w, R, 0, "role", abi.LEADER)
+    set_fld(w, R, 0, "flags", abi.FL_HB_ACTIVE)
+    set_fld(w, R, 0, "last", 3)
+    set_fld(w, R, 0, "phys", 3)
+    set_session(w, R, 0, [1] * R, [0] * R)
+    e.write_state(w)
+    t = np.zeros((1, R, 64), np.int32)
+    c = np.zeros((1, R, 64), np.uint32)
+    t[0, 0, :3] = 1
+    c[0, 0, :3] = ids
+    e.write_log(t, c)
+    assert svc.node(0, 0).entries() == ["1: a", "1: b", "1: c"]
+    e.step(1)
+    assert svc.node(0, 0).entries() == ["1: a"]                  # self-append truncated the leader (K7)
+    e.step(1)
+    assert svc.node(0, 0).appendCommand("d") == "d"
+    assert svc.node(0, 0).entries() == ["1: a", "1: b"]          # `d` went to the physical end
+    e.step(1)
+    for r in range(R):
+        assert svc.node(0, r).entries() == ["1: a", "1: b"], r
+
+    kw = dict(abi.CONFIGS[2], G=200)
+    e2, o2 = pair(log_cap=200, **kw)
+    e2.step(150)
+    o2.step(150)
+    svc2 = service_mod.RaftService(e2)
+    so = o2.read_state()
+    ot, oc = o2.read_log()
+    for g in range(0, 200, 37):
+        for r in range(3):
+            last = int(fld(so[g], 3, r, "last"))
+            want = [f"{int(ot[g, r, j])}: {svc2.commands.name(oc[g, r, j])}" for j in range(last)]
+            assert svc2.node(g, r).entries() == want, (g, r)
+            assert last == 0 or want[0].startswith(f"{int(ot[g, r, 0])}: cmd#")

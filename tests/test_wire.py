@@ -158,3 +158,19 @@ def test_empty_batches():
     assert wire.decode_vote_requests([]).shape == (0, 4)
     assert wire.encode_vote_responses(np.zeros((0, 2), np.int32)) == []
     assert wire.encode_vote_requests(np.zeros((1, 4), np.int32)) == [b""]
+
+
+def test_worst_case_append_requests_fit_the_encoder_buffer(pb):
+    """Every int32 field negative (10-byte varints) and a negative entry term:
+    about 80 bytes before the command.  The wrapper's buffer bound must hold
+    for a whole batch of them (64 B per message did not)."""
+    n = 50
+    req = np.tile(np.array([-1, -2**31, -5, -7, 1, -3, 0, -2**31], np.int32), (n, 1))
+    cmds = [b"x" * (m % 3) for m in range(n)]
+    enc = wire.encode_append_requests(req, cmds)
+    M = pb["RequestAppendEntriesRPC"]
+    for m, b in enumerate(enc):
+        x = M.FromString(b)
+        assert (x.term, x.prevLogIndex, x.leaderCommit) == (-1, -5, -2**31)
+        assert x.entries[0].term == -3 and x.entries[0].command == cmds[m].decode()
+        assert len(b) > 64                                 # beyond the old per-message bound
