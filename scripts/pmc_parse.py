@@ -35,6 +35,17 @@ def dispatches(d):
     return {c: [v for _, v in sorted(x.items())] for c, x in acc.items()}
 
 
+def traced_ms(d):
+    """[duration ms per step_kernel dispatch, in dispatch order] from the
+    --kernel-trace run of the same command (empty if absent)."""
+    rows = []
+    for f in glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True):
+        for row in csv.DictReader(open(f)):
+            if "step_kernel" in row["Kernel_Name"]:
+                rows.append((int(row["Dispatch_Id"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
+    return [v for _, v in sorted(rows)]
+
+
 def mean(xs):
     return sum(xs) / len(xs) if xs else None
 
@@ -53,6 +64,7 @@ def main(d):
             if len(vals) != len(seq):
                 raise SystemExit(f"{p}: {len(vals)} step_kernel dispatches, plan has {len(seq)}")
             per[c] = vals
+    tr = traced_ms(d)
     rows = []
     for leg in ("timed", "streaming"):
         ix = [i for i, (lg, _) in enumerate(seq) if lg == leg]
@@ -77,6 +89,9 @@ def main(d):
             "waves": m.get("SQ_WAVES"), "wave_cycles": m.get("SQ_WAVE_CYCLES"),
             "busy_cycles": m.get("SQ_BUSY_CYCLES"), "active_inst_valu": m.get("SQ_ACTIVE_INST_VALU"),
             "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"), "launches_averaged": len(ix),
+            "trace_avg_ms": mean([tr[i] for i in ix]) if len(tr) == len(seq) else None,
+            "effective_clock_ghz": (m["GRBM_GUI_ACTIVE"] / 8 / (mean([tr[i] for i in ix]) / 1e3) / 1e9
+                                    if len(tr) == len(seq) and m.get("GRBM_GUI_ACTIVE") else None),
             "source": f"rocprofv3 --pmc, separate passes (scripts/pmc_bench.sh, {os.path.basename(d)})",
         })
         rows.append(row)

@@ -186,3 +186,13 @@ def test_k7_leader_self_truncation():
     for r in (1, 2):
         assert fld(s, R, r, "last") == 2
         assert [int(c[0, r, j]) for j in range(2)] == [a, b]
+
+
+# ---- K8-K14: the election loop and the remaining quirks (tests/kats_election.py) ----
+import kats_election as KE  # noqa: E402
+
+
+@pytest.mark.parametrize("kat", KE.KATS, ids=lambda k: k["name"].split()[0])
+def test_election_kats_on_oracle(kat):
+    o = O.Oracle(abi.make_params(**KE.params(kat["R"])))
+    KE.run(kat, o)
