@@ -203,6 +203,10 @@ def parse_args(argv=None):
     ap.add_argument("--stream-steps", type=int, default=200,
                     help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
+    ap.add_argument("--log-window", type=int, default=-1,
+                    help="ring slots per replica (power of two; 0 = keep every physical slot); default: 256 for "
+                         "configs 2 and 3, whose log accesses stay within 48 slots of physLen, 0 for config 5, "
+                         "whose ghost-tail gaps reach thousands of slots (DESIGN.md §4.2)")
     ap.add_argument("--reduce-every", type=int, default=512,
                     help="steps per counter all-reduce (rounded to whole launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -324,10 +328,13 @@ def main():
     # physical slots a replica can fill: ~0.3 per step at config 3's command
     # rate, up to one per step where every leader takes a command each step
     log_cap = args.log_cap or int(64 + (1.0 if kw["cmd_ppm"] >= 1_000_000 else 0.3) * total_steps)
+    window = args.log_window if args.log_window >= 0 else {2: 256, 3: 256, 5: 0}[args.config]
+    log_cap = max(log_cap, window)                          # the window never exceeds the physLen limit
     L = launch_length(args.steps, args.steps_per_launch)   # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
     mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
-    params = abi.make_params(log_cap=log_cap, steps_per_launch=L, mode=mode, **dict(kw, G=G_local, g0=g0))
+    params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode,
+                             **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
@@ -402,8 +409,9 @@ def main():
     achieved = bytes_alg / kern_s / 1e9 if launches else 0.0
     achieved_state = bytes_state / kern_s / 1e9 if launches else 0.0
     overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
+    wmiss = int(c_all[:, abi.C_INDEX["log_window_miss"]].sum())
     pmc_key = {"config": args.config, "mode": args.mode, "groups": G_local, "launch_steps": L,
-               "warmup": args.warmup, "steps": args.steps}
+               "warmup": args.warmup, "steps": args.steps, "log_window": window}
     pmc = load_pmc(dict(pmc_key, leg="timed")) if len(set(timed_plan)) == 1 else None
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     roofline_valu = None
@@ -469,6 +477,7 @@ def main():
         "commit_regressions": int(c_all[:, abi.C_INDEX["commit_regressions"]].sum()),
         "dual_leader_group_steps": int(c_all[:, abi.C_INDEX["dual_leader_groups"]].sum()),
         "log_overflow": overflow,
+        "log_window_misses": wmiss,
         "note": "observations of the reference's protocol (quirks Q4/Q9 do not preserve these "
                 "properties); over the timed steps, Log Matching at the end of the run",
     }
@@ -495,6 +504,7 @@ def main():
                            2: ", no faults, 1/4 command per group-step"}[args.config]
                         + (", textbook mode" if mode else ""),
             "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
+            "log_window": window, "hbm_bytes_engine": eng.device_bytes,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
             "counter_allreduce_every": chunk if world > 1 else None,
         },
@@ -519,7 +529,7 @@ def main():
         },
         "roofline_valu": roofline_valu,
         "roofline_streaming": streaming,
-        "valid": overflow == 0,
+        "valid": overflow == 0 and wmiss == 0,
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }

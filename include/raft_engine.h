@@ -49,6 +49,8 @@ extern "C" {
 #define RAFT_EDEVICE      -3   /* HIP runtime error                          */
 #define RAFT_ERANGE       -4   /* group range outside the engine             */
 #define RAFT_ENODEV       -5   /* no HIP device / kernel image unavailable   */
+#define RAFT_EWINDOW      -6   /* a handler batch touched a log slot below the
+                                * retained window (results invalid, like overflow) */
 
 /* ---- node roles: enum class State (RaftServer.kt:24-26) --------------- */
 #define RAFT_FOLLOWER  0
@@ -100,7 +102,14 @@ typedef struct raft_params {
     int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
     int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch, 0..RAFT_MAX_STEPS_PER_LAUNCH (0 = 1) */
     int32_t  mode;              /* RAFT_MODE_* (0 = the reference)                                  */
-    int32_t  reserved[6];
+    int32_t  log_window;        /* 0 = every physical slot is kept (log_cap slots per replica);
+                                 * else a power of two W <= log_cap: only the newest W physical
+                                 * slots [physLen - W, physLen) of each replica are kept, in a ring
+                                 * (DESIGN.md §4.2).  Every Log.get / Log.add of the reference below
+                                 * physLen - W is counted in RAFT_C_LOG_WINDOW_MISS; a run with a
+                                 * miss is invalid (its results are not the reference's), as with
+                                 * RAFT_C_LOG_OVERFLOW.  log_cap stays the physLen limit.          */
+    int32_t  reserved[5];
 } raft_params;
 
 /* ---- per-step counters (sum over the engine's groups) ------------------ */
@@ -126,6 +135,7 @@ enum raft_counter {
     RAFT_C_PREV_READS_FOLLOWER, /* P_F: log[prev].term reads in append()                        */
     RAFT_C_ENTRY_WRITES,        /* E_W: Log.add stores from append()                            */
     RAFT_C_VOTE_LOG_READS,      /* V: last-log-term reads in the vote path                      */
+    RAFT_C_LOG_WINDOW_MISS,     /* Log.get/Log.add below physLen - log_window (run invalid)      */
     RAFT_NUM_COUNTERS
 };
 #define RAFT_COUNTER_STRIDE 32  /* int64 slots per step in counter buffers */
@@ -223,17 +233,23 @@ int64_t raft_engine_device_bytes(raft_engine* e); /* HBM owned by the engine */
 /* out: [n][raft_group_words(R)] int32, canonical layout above. */
 int raft_engine_read_state(raft_engine* e, int64_t g0, int64_t n, int32_t* out);
 int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t* in);
-/* terms/cmds: [n][R][log_cap]; slots >= physLen are unspecified. */
+/* terms/cmds: [n][R][log_cap], physical slot j at [j]; slots >= physLen are
+ * unspecified, and with a log_window W the slots below physLen - W read as 0
+ * and are not written. */
 int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds);
 int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds);
-/* Order-independent 64-bit digest of the full canonical state (logs to
- * physLen included): sum over groups of a per-group hash. */
+/* Order-independent 64-bit digest of the full canonical state and the
+ * retained log slots [max(0, physLen - W), physLen) of every replica (W =
+ * log_window, or every slot): sum over groups of a per-group hash (DESIGN.md
+ * §3 S-13).  digest_range hashes groups [g0, g0 + n) only. */
 int raft_engine_digest(raft_engine* e, uint64_t* out);
+int raft_engine_digest_range(raft_engine* e, int64_t g0, int64_t n, uint64_t* out);
 
 /* Log Matching over committed prefixes (safety flag): a
  * group of [g0, g0+n) is flagged when two of its replicas hold different
  * (term, cmd) at an index inside both replicas' committed prefixes, i.e.
- * i < min(commitIndex, lastIndex) of each.  The reference's quirks (Q4 commit
+ * i < min(commitIndex, lastIndex) of each (and, with a log_window, inside
+ * both replicas' retained windows).  The reference's quirks (Q4 commit
  * clamp, Q9 no current-term guard) do not preserve this property, so the
  * count is an observation about the reference's protocol, not an engine
  * error.  *mismatched = flagged groups; flags (nullable, host, n bytes)
@@ -243,7 +259,9 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
 /* ---- single-handler batches: the service boundary ----------------------
  * group: engine-local group index; dst: replica index 0..R-1.  Messages
  * to the same (group, dst) are applied in batch order.  Effects on the
- * consumer (timer reset) use the engine's current step index. */
+ * consumer (timer reset) use the engine's current step index.  With a
+ * log_window, a batch in which some handler touched a slot below its
+ * replica's window returns RAFT_EWINDOW after applying it. */
 int raft_vote_batch(raft_engine* e, const int64_t* group, const int32_t* dst,
                     const raft_vote_req* req, raft_vote_resp* resp, int64_t n);
 int raft_append_batch(raft_engine* e, const int64_t* group, const int32_t* dst,

@@ -49,6 +49,8 @@ def lib():
             "oracle_read_log": (C.c_int, [o, I64, I64, P(I32), P(U32)]),
             "oracle_write_log": (C.c_int, [o, I64, I64, P(I32), P(U32)]),
             "oracle_digest": (C.c_uint64, [o]),
+            "oracle_digest_range": (C.c_uint64, [o, I64, I64]),
+            "oracle_set_log_window": (C.c_int, [o, I32]),
             "oracle_vote": (C.c_int, [o, I64, I32, P(abi.raft_vote_req), P(abi.raft_vote_resp)]),
             "oracle_append": (C.c_int, [o, I64, I32, P(abi.raft_append_req), P(abi.raft_append_resp)]),
             "oracle_append_command": (C.c_int, [o, I64, I32, U32]),
@@ -186,6 +188,14 @@ class Oracle:
 
     def digest(self) -> int:
         return int(lib().oracle_digest(self.h))
+
+    def digest_range(self, g0: int, n: int) -> int:
+        return int(lib().oracle_digest_range(self.h, g0, n))
+
+    def set_log_window(self, w: int):
+        """View every log through a log_window of w slots (0: all); the lists keep every slot."""
+        if lib().oracle_set_log_window(self.h, int(w)) != 0:
+            raise ValueError(w)
 
     def vote(self, group, dst, term, candidate_id, last_log_index, last_log_term):
         rq = abi.raft_vote_req(term, candidate_id, last_log_index, last_log_term)

@@ -34,8 +34,18 @@ typedef struct {
     int32_t  alloc;
     int32_t  cap;         /* build-side physical capacity; overflow counted       */
     int32_t  textbook;    /* RAFT_MODE_TEXTBOOK: array semantics, no ghost tail   */
+    int32_t  window;      /* build-side log_window W (0: every slot kept); the    *
+                           * oracle keeps the whole list and counts accesses      *
+                           * below size - W (RAFT_C_LOG_WINDOW_MISS)              */
     entry_t* items;
 } olog_t;
+
+/* An access of the reference (Log.get / Log.add) at physical index j that a
+ * W-slot window would not hold: j < size - W.  Counted, never served
+ * differently: the run is invalid, as with overflow. */
+static void olog_touch(const olog_t* l, int32_t j, int64_t* c) {
+    if (c && l->window && j < l->size - l->window) c[RAFT_C_LOG_WINDOW_MISS]++;
+}
 
 /* Commons.kt:53-54: get(i) = if (lastIndex - 1 < i) throw IndexOutOfBounds else log[i]
  * (log[i] itself throws for i < 0).  Returns 0 where the reference throws. */
@@ -59,11 +69,13 @@ static int olog_reserve(olog_t* l, int32_t n) {
 }
 
 /* Commons.kt:56-68.  Returns 1 (true), 0 (false), -1 (build-side overflow:
- * no physical slot left, nothing changes), -2 (ArrayList.set threw, i < 0). */
-static int olog_add(olog_t* l, int32_t i, entry_t e) {
+ * no physical slot left, nothing changes), -2 (ArrayList.set threw, i < 0).
+ * c: the step's counters (window misses), or NULL. */
+static int olog_add(olog_t* l, int32_t i, entry_t e, int64_t* c) {
     if (l->textbook && i >= 0 && i <= l->lastIndex) {
         /* textbook mode: an array log -- slot i, truncating after it (no ghost tail, Q1) */
         if (i >= l->cap) return -1;
+        olog_touch(l, i, c);
         olog_reserve(l, i + 1);
         l->items[i] = e;
         l->lastIndex = i + 1;
@@ -80,6 +92,7 @@ static int olog_add(olog_t* l, int32_t i, entry_t e) {
         return 0;
     } else {                                       /* :63-66 */
         if (i < 0) return -2;
+        olog_touch(l, i, c);
         l->items[i] = e;                           /* :64 log[i] = entry (no shrink: ghost tail) */
         l->lastIndex = i + 1;                      /* :65 */
         return 1;
@@ -231,6 +244,7 @@ static void build_vote_request(const ctx_t* x, onode_t* n) {
     else {
         entry_t e = { 0, 0 };
         olog_get(&n->log, n->log.lastIndex - 1, &e);
+        olog_touch(&n->log, n->log.lastIndex - 1, x->c);
         n->reqLastTerm = e.term;
         x->c[RAFT_C_VOTE_LOG_READS]++;
     }
@@ -282,6 +296,7 @@ static void vote_handler(const ctx_t* x, onode_t* n, const raft_vote_req* rq, ra
             entry_t last = { 0, 0 };
             if (n->log.lastIndex >= 1) {
                 olog_get(&n->log, n->log.lastIndex - 1, &last);
+                olog_touch(&n->log, n->log.lastIndex - 1, x->c);
                 x->c[RAFT_C_VOTE_LOG_READS]++;
             }
             granted = !(n->log.lastIndex >= 1 && (rq->last_log_term < last.term ||
@@ -297,6 +312,7 @@ static void vote_handler(const ctx_t* x, onode_t* n, const raft_vote_req* rq, ra
         entry_t last = { 0, 0 };
         if (n->log.lastIndex >= 1) {
             olog_get(&n->log, n->log.lastIndex - 1, &last);
+            olog_touch(&n->log, n->log.lastIndex - 1, x->c);
             x->c[RAFT_C_VOTE_LOG_READS]++;
         }
         if (n->log.lastIndex >= 1 && rq->last_log_term < last.term) granted = 0;          /* :232-233 */
@@ -346,6 +362,7 @@ static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq,
             rs->term = n->currentTerm; rs->success = 0; rs->status = 1;
             return 1;
         }
+        olog_touch(&n->log, rq->prev_log_index, x->c);
         x->c[RAFT_C_PREV_READS_FOLLOWER]++;
         success = (pe.term == rq->prev_log_term);
     } else success = 0;
@@ -353,10 +370,12 @@ static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq,
     if (success && rq->has_entry) {                /* :278 (Q2, Q10) */
         entry_t e = { rq->entry_term, rq->entry_cmd }, cur;
         const int32_t i = rq->prev_log_index + 1;
-        if (tb && i < n->log.lastIndex && olog_get(&n->log, i, &cur) && cur.term == e.term) {
+        const int have = tb && i < n->log.lastIndex && olog_get(&n->log, i, &cur);
+        if (have) olog_touch(&n->log, i, x->c);
+        if (have && cur.term == e.term) {
             stored = 1;                            /* textbook: no conflict, no truncation */
         } else {
-            int r = olog_add(&n->log, i, e);
+            int r = olog_add(&n->log, i, e, x->c);
             if (r == 1) { x->c[RAFT_C_ENTRY_WRITES]++; stored = 1; }
             else if (r == -1) x->c[RAFT_C_LOG_OVERFLOW]++;
         }
@@ -376,7 +395,7 @@ static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq,
 /* appendCommand(command) (RaftServer.kt:100-107) */
 static void append_command(const ctx_t* x, onode_t* n, uint32_t cmd) {
     entry_t e = { n->currentTerm, cmd };           /* :101-104 */
-    int r = olog_add(&n->log, n->log.lastIndex, e);/* :105 */
+    int r = olog_add(&n->log, n->log.lastIndex, e, x->c);   /* :105 */
     x->c[RAFT_C_COMMANDS]++;
     if (r == -1) x->c[RAFT_C_LOG_OVERFLOW]++;
 }
@@ -506,12 +525,12 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
             ok[d] = 1;
             if (prev >= 0) {                       /* :128 */
                 if (!olog_get(&L->log, prev, &pe)) ok[d] = 0;       /* Q11: throws, caught :170 */
-                else { prevTerm = pe.term; c[RAFT_C_PREV_READS_LEADER]++; }
+                else { prevTerm = pe.term; c[RAFT_C_PREV_READS_LEADER]++; olog_touch(&L->log, prev, c); }
             }
             int has = 0;
             if (ok[d] && L->log.lastIndex >= L->nextIndex[d]) {     /* :130 */
                 if (!olog_get(&L->log, i - 1, &ent)) ok[d] = 0;     /* :131 */
-                else { has = 1; c[RAFT_C_ENTRY_READS_LEADER]++; }
+                else { has = 1; c[RAFT_C_ENTRY_READS_LEADER]++; olog_touch(&L->log, i - 1, c); }
             }
             if (!ok[d]) { c[RAFT_C_APPEND_SKIPPED]++; continue; }
             rq[d].term = L->currentTerm;           /* :137-143 */
@@ -581,7 +600,9 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
                 for (int b = a; b > 0 && m[b] > m[b - 1]; --b) { int32_t v = m[b]; m[b] = m[b - 1]; m[b - 1] = v; }
             const int32_t N = m[maj - 1];
             entry_t ne;
-            if (N > L->commitIndex && olog_get(&L->log, N - 1, &ne) && ne.term == L->currentTerm) {
+            const int got = N > L->commitIndex && olog_get(&L->log, N - 1, &ne);
+            if (got) olog_touch(&L->log, N - 1, c);
+            if (got && ne.term == L->currentTerm) {
                 L->commitIndex = N;
                 c[RAFT_C_COMMITS]++;
             }
@@ -626,6 +647,7 @@ static void init_group(const struct oracle* o, ogroup_t* g, uint32_t gid) {
         n->state = RAFT_FOLLOWER;                  /* :42 */
         n->log.cap = o->p.log_cap;
         n->log.textbook = o->p.mode == RAFT_MODE_TEXTBOOK;
+        n->log.window = o->p.log_window;
         reset_timer(&x, n);                        /* init: ResettableCountdownTimer(...) starts (:58, Commons.kt:14) */
     }
 }
@@ -633,7 +655,8 @@ static void init_group(const struct oracle* o, ogroup_t* g, uint32_t gid) {
 int oracle_create(const raft_params* p, oracle_t** out) {
     if (!p || !out || p->R < 1 || p->R > MAXR || p->G < 1 || p->log_cap < 1 || p->heartbeat_ms <= 0 ||
         p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms ||
-        (p->mode != RAFT_MODE_REFERENCE && p->mode != RAFT_MODE_TEXTBOOK))
+        (p->mode != RAFT_MODE_REFERENCE && p->mode != RAFT_MODE_TEXTBOOK) || p->log_window < 0 ||
+        (p->log_window && ((p->log_window & (p->log_window - 1)) || p->log_window > p->log_cap)))
         return RAFT_EINVAL;
     oracle_t* o = (oracle_t*)calloc(1, sizeof(*o));
     if (!o) return RAFT_ENOMEM;
@@ -816,9 +839,11 @@ int oracle_read_log(const oracle_t* o, int64_t g0, int64_t n, int32_t* terms, ui
         for (int r = 0; r < o->R; ++r) {
             const olog_t* l = &o->groups[g0 + i].n[r].log;
             size_t base = ((size_t)i * o->R + r) * (size_t)cap;
-            for (int64_t j = 0; j < cap; ++j) {
-                terms[base + j] = j < l->size ? l->items[j].term : 0;
-                cmds[base + j] = j < l->size ? l->items[j].cmd : 0;
+            const int64_t lo = l->window && l->size > l->window ? l->size - l->window : 0;
+            for (int64_t j = 0; j < cap; ++j) {       /* the retained window only, like the engine */
+                const int in = j >= lo && j < l->size;
+                terms[base + j] = in ? l->items[j].term : 0;
+                cmds[base + j] = in ? l->items[j].cmd : 0;
             }
         }
     return RAFT_OK;
@@ -831,9 +856,10 @@ int oracle_write_log(oracle_t* o, int64_t g0, int64_t n, const int32_t* terms, c
         for (int r = 0; r < o->R; ++r) {
             olog_t* l = &o->groups[g0 + i].n[r].log;
             size_t base = ((size_t)i * o->R + r) * (size_t)cap;
-            for (int32_t j = 0; j < l->size; ++j) {
-                l->items[j].term = terms[base + j];
-                l->items[j].cmd = cmds[base + j];
+            const int32_t lo = l->window && l->size > l->window ? l->size - l->window : 0;
+            for (int32_t j = 0; j < l->size; ++j) {   /* below the window: 0, as the engine reads it */
+                l->items[j].term = j >= lo ? terms[base + j] : 0;
+                l->items[j].cmd = j >= lo ? cmds[base + j] : 0;
             }
         }
     return RAFT_OK;
@@ -850,12 +876,26 @@ static uint64_t fmix64(uint64_t k) {
 }
 #define FEED(h, v) do { (h) ^= (uint32_t)(v); (h) *= 0x100000001b3ull; } while (0)
 
-uint64_t oracle_digest(const oracle_t* o) {
+uint64_t oracle_digest(const oracle_t* o) { return oracle_digest_range(o, 0, o->G); }
+
+/* Change the log_window every replica's log is viewed through (digest,
+ * read_log, miss counting); the lists themselves always hold every slot. */
+int oracle_set_log_window(oracle_t* o, int32_t w) {
+    if (!o || w < 0 || (w & (w - 1)) || w > o->p.log_cap) return RAFT_EINVAL;
+    o->p.log_window = w;
+    for (int64_t g = 0; g < o->G; ++g)
+        for (int r = 0; r < o->R; ++r) o->groups[g].n[r].log.window = w;
+    return RAFT_OK;
+}
+
+uint64_t oracle_digest_range(const oracle_t* o, int64_t g0, int64_t n) {
     const int R = o->R;
     const int32_t W = raft_group_words(R);
     int32_t* w = (int32_t*)malloc((size_t)W * sizeof(int32_t));
     uint64_t total = 0;
-    for (int64_t g = 0; g < o->G; ++g) {
+    if (g0 < 0) g0 = 0;
+    if (g0 + n > o->G) n = o->G - g0;
+    for (int64_t g = g0; g < g0 + n; ++g) {
         const ogroup_t* gr = &o->groups[g];
         export_group(o, gr, w);
         uint64_t gid = (uint64_t)(o->p.g0 + g);
@@ -865,7 +905,8 @@ uint64_t oracle_digest(const oracle_t* o) {
             for (int d = 0; d < R; ++d) FEED(h, w[R * RAFT_NUM_FIELDS + r * R + d]);
             for (int d = 0; d < R; ++d) FEED(h, w[R * RAFT_NUM_FIELDS + R * R + r * R + d]);
             const olog_t* l = &gr->n[r].log;
-            for (int32_t j = 0; j < l->size; ++j) { FEED(h, l->items[j].term); FEED(h, l->items[j].cmd); }
+            const int32_t lo = l->window && l->size > l->window ? l->size - l->window : 0;
+            for (int32_t j = lo; j < l->size; ++j) { FEED(h, l->items[j].term); FEED(h, l->items[j].cmd); }
         }
         FEED(h, w[W - 2]);
         FEED(h, w[W - 1]);
@@ -914,7 +955,7 @@ oracle_log_t* oracle_log_new(int32_t cap) {
 void oracle_log_free(oracle_log_t* x) { if (x) { free(x->l.items); free(x); } }
 int32_t oracle_log_add(oracle_log_t* x, int32_t i, int32_t term, uint32_t cmd) {
     entry_t e = { term, cmd };
-    return olog_add(&x->l, i, e);
+    return olog_add(&x->l, i, e, NULL);
 }
 int32_t oracle_log_get(const oracle_log_t* x, int32_t i, int32_t* term, uint32_t* cmd) {
     entry_t e;

@@ -31,6 +31,8 @@ int  oracle_write_state(oracle_t* o, int64_t g0, int64_t n, const int32_t* in);
 int  oracle_read_log(const oracle_t* o, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds);
 int  oracle_write_log(oracle_t* o, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds);
 uint64_t oracle_digest(const oracle_t* o);
+uint64_t oracle_digest_range(const oracle_t* o, int64_t g0, int64_t n);
+int oracle_set_log_window(oracle_t* o, int32_t w);
 
 /* single handlers, same semantics as raft_vote_batch & co (applied in order) */
 int oracle_vote(oracle_t* o, int64_t group, int32_t dst, const raft_vote_req* req, raft_vote_resp* resp);

@@ -22,6 +22,7 @@ RAFT_ENOMEM = -2
 RAFT_EDEVICE = -3
 RAFT_ERANGE = -4
 RAFT_ENODEV = -5
+RAFT_EWINDOW = -6
 
 # enum class State (RaftServer.kt:24-26)
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
@@ -37,7 +38,7 @@ COUNTER_NAMES = [
     "leaders_elected", "sessions_ticked", "append_sent", "append_skipped",
     "entries_acked", "commits", "msg_dropped", "commands", "commit_regressions",
     "dual_leader_groups", "log_overflow", "prev_reads_leader",
-    "entry_reads_leader", "prev_reads_follower", "entry_writes", "vote_log_reads",
+    "entry_reads_leader", "prev_reads_follower", "entry_writes", "vote_log_reads", "log_window_miss",
 ]
 NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
@@ -66,7 +67,8 @@ class raft_params(C.Structure):
         ("drop_ppm", C.c_uint32), ("churn_ppm", C.c_uint32), ("churn_steps", C.c_int32),
         ("partition_period", C.c_int32), ("partition_len", C.c_int32),
         ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
-        ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("reserved", C.c_int32 * 6),
+        ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("log_window", C.c_int32),
+        ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -180,6 +182,7 @@ def load_library(path: str | None = None):
         "raft_engine_read_log": (C.c_int, [eng, I64, I64, P(I32), P(C.c_uint32)]),
         "raft_engine_write_log": (C.c_int, [eng, I64, I64, P(I32), P(C.c_uint32)]),
         "raft_engine_digest": (C.c_int, [eng, P(U64)]),
+        "raft_engine_digest_range": (C.c_int, [eng, I64, I64, P(U64)]),
         "raft_engine_check_log_matching": (C.c_int, [eng, I64, I64, P(C.c_uint8), P(I64)]),
         "raft_vote_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_vote_req), P(raft_vote_resp), I64]),
         "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
@@ -213,7 +216,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
-    "raft_engine_write_log", "raft_engine_digest", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
+    "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_philox4x32_10",
     # include/raft_wire.h
     "raft_wire_decode_vote_req", "raft_wire_encode_vote_req", "raft_wire_decode_vote_resp",

@@ -186,7 +186,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
     c.gg0 = (uint32_t)(p.g0 + c.wg0);
     const int64_t idx = g * R + r;
-    c.lr = p.log + (live ? idx : 0) * (int64_t)p.cap;
+    c.lr = p.log + (live ? idx : 0);
     c.iso = -1;
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
@@ -258,14 +258,20 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     }
 }
 
+__device__ __forceinline__ LogView log_of(const DevParams& p, int64_t idx) {
+    return LogView{p.log + idx, p.wmask, (uint32_t)p.GR, p.cap, p.W};
+}
+// the retained physical slots of a replica: [max(0, physLen - W), physLen)
+__device__ __forceinline__ int32_t window_lo(const DevParams& p, int32_t phys) { return max(0, phys - p.W); }
+
 // (re)derive the log-tail cache from lastIndex and the log (after host writes)
 __global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
     const int64_t idx = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (idx >= p.GR) return;
     const int32_t last = p.st[fidx(p, RAFT_F_LAST, idx)];
-    const uint2* lr = p.log + idx * (int64_t)p.cap;
-    const uint2 a = last >= 1 ? lr[last - 1] : make_uint2(0u, 0u);
-    const uint2 b = last >= 2 ? lr[last - 2] : make_uint2(0u, 0u);
+    const LogView lv = log_of(p, idx);
+    const uint2 a = last >= 1 ? *lv.at(last - 1) : make_uint2(0u, 0u);
+    const uint2 b = last >= 2 ? *lv.at(last - 2) : make_uint2(0u, 0u);
     p.st[fidx(p, F_T1, idx)] = (int32_t)a.x;
     p.st[fidx(p, F_C1, idx)] = (int32_t)a.y;
     p.st[fidx(p, F_T2, idx)] = (int32_t)b.x;
@@ -364,23 +370,25 @@ __global__ __launch_bounds__(BLOCK) void log_match_kernel(DevParams p, int64_t g
     const int64_t k = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
     if (k >= n) return;                                                   // wave-uniform
     const int64_t g = g0 + k;
-    int32_t c[R];
-    int32_t cmax = 0;
+    int32_t c[R], lo[R];
+    int32_t cmax = 0, lmin = 0x7FFFFFFF;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t idx = g * R + r;
         const int32_t cm = min(p.st[fidx(p, RAFT_F_COMMIT, idx)], p.st[fidx(p, RAFT_F_LAST, idx)]);
         c[r] = max(0, min(cm, p.cap));
+        lo[r] = window_lo(p, p.st[fidx(p, RAFT_F_PHYS, idx)]);     // retained slots only
         cmax = max(cmax, c[r]);
+        lmin = min(lmin, lo[r]);
     }
     bool bad = false;
-    for (int32_t i = lane; i < cmax; i += 64) {
+    for (int32_t i = lmin + lane; i < cmax; i += 64) {
         bool have = false;
         uint2 ref = make_uint2(0u, 0u);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            if (i < c[r]) {
-                const uint2 v = p.log[(g * R + r) * (int64_t)p.cap + i];
+            if (i < c[r] && i >= lo[r]) {
+                const uint2 v = *log_of(p, g * R + r).at(i);
                 bad |= have && (v.x != ref.x || v.y != ref.y);
                 ref = have ? ref : v;
                 have = true;
@@ -395,11 +403,11 @@ __global__ __launch_bounds__(BLOCK) void log_match_kernel(DevParams p, int64_t g
 }
 
 template <int R>
-__global__ __launch_bounds__(BLOCK) void digest_kernel(DevParams p, unsigned long long* out) {
+__global__ __launch_bounds__(BLOCK) void digest_kernel(DevParams p, int64_t g0, int64_t n, unsigned long long* out) {
     __shared__ unsigned long long part[WAVES_PER_BLOCK];
-    const int64_t g = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const int64_t g = g0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     uint64_t hv = 0;
-    if (g < p.G) {
+    if (g < g0 + n) {
         uint64_t h = 0xcbf29ce484222325ull ^ ((uint64_t)(p.g0 + g) * 0x9E3779B97F4A7C15ull);
         auto feed = [&](int32_t v) { h ^= (uint32_t)v; h *= 0x100000001b3ull; };
         const int s0 = p.gx[GX_S0 * p.G + g];
@@ -412,8 +420,12 @@ __global__ __launch_bounds__(BLOCK) void digest_kernel(DevParams p, unsigned lon
             for (int d = 0; d < R; ++d) feed(canon_next(p, R, g, s0, r, d));
             for (int d = 0; d < R; ++d) feed(canon_match(p, R, g, s0, r, d));
             const int32_t phys = p.st[fidx(p, RAFT_F_PHYS, idx)];
-            const uint2* lr = p.log + idx * (int64_t)p.cap;
-            for (int32_t q = 0; q < phys; ++q) { const uint2 e = lr[q]; feed((int32_t)e.x); feed((int32_t)e.y); }
+            const LogView lv = log_of(p, idx);
+            for (int32_t q = window_lo(p, phys); q < phys; ++q) {
+                const uint2 e = *lv.at(q);
+                feed((int32_t)e.x);
+                feed((int32_t)e.y);
+            }
         }
         feed(p.gx[GX_ISO * p.G + g]);
         feed(p.gx[GX_CMDS * p.G + g]);
@@ -456,11 +468,11 @@ __device__ __forceinline__ void load_rep(RepState& x, const DevParams& p, int64_
 }
 
 // the batch path derives the tail cache from the log (the HBM copy may be stale)
-__device__ __forceinline__ void derive_cache(RepState& x, const uint2* lr) {
-    const uint2 a = x.last >= 1 ? lr[x.last - 1] : make_uint2(0u, 0u);
+__device__ __forceinline__ void derive_cache(RepState& x, const LogView& lv) {
+    const uint2 a = x.last >= 1 ? *lv.at(x.last - 1) : make_uint2(0u, 0u);
     x.t1 = (int32_t)a.x;
     x.c1 = a.y;
-    x.t2 = x.last >= 2 ? (int32_t)lr[x.last - 2].x : 0;
+    x.t2 = x.last >= 2 ? (int32_t)lv.at(x.last - 2)->x : 0;
 }
 
 __device__ __forceinline__ void store_rep(const RepState& x, const DevParams& p, int64_t idx) {
@@ -481,11 +493,21 @@ __device__ __forceinline__ void resolve_rep_draw(RepState& x, const DevParams& p
 
 enum { BATCH_VOTE = 0, BATCH_APPEND = 1, BATCH_COMMAND = 2 };
 
+// The batch handlers report one thing: reference accesses below the window
+// (the run is then invalid, RAFT_EWINDOW).  Called in divergent control flow:
+// a mask's bit for this lane is read with ib().
+struct BatchCounters {
+    uint32_t miss = 0;
+    __device__ __forceinline__ void add(uint64_t m, int c) {
+        if (c == RAFT_C_LOG_WINDOW_MISS) miss += ib(m) ? 1u : 0u;
+    }
+};
+
 // keys[k] = group * R + replica; msgs of key k are order[off[k] .. off[k+1])
 template <bool TB>
 __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int nkeys,
                                                       const int64_t* keys, const int64_t* off, const int64_t* order,
-                                                      const void* req, void* resp) {
+                                                      const void* req, void* resp, unsigned int* misses) {
     const int k = blockIdx.x * BLOCK + threadIdx.x;
     if (k >= nkeys) return;
     const int R = p.R;
@@ -495,9 +517,9 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
     const uint32_t gid = (uint32_t)(p.g0 + i);
     RepState x;
     load_rep(x, p, idx);
-    uint2* lr = p.log + idx * (int64_t)p.cap;
-    derive_cache(x, lr);
-    NoCounters cnt;
+    const LogView lv = log_of(p, idx);
+    derive_cache(x, lv);
+    BatchCounters cnt;
     for (int64_t m = off[k]; m < off[k + 1]; ++m) {
         const int64_t o = order[m];
         if (kind == BATCH_VOTE) {
@@ -505,26 +527,47 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             int32_t rt;
             uint64_t gr;
             vote_handler<TB>(x.ref(), __ballot(1), r + 1, q.term, q.candidate_id, q.last_log_index, q.last_log_term,
-                             cnt, rt, gr);
+                             p.W, cnt, rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
             int32_t rt = 0;
             uint64_t su = 0;
             const int32_t pv = q.prev_log_index;
-            const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lr[pv].x : 0;
-            const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lr[pv + 1].x : 0;
-            const uint64_t thrown = append_handler<TB>(x.ref(), __ballot(1), r + 1, lr, p.cap, q.term, q.leader_id, pv,
+            const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
+            const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
+            const uint64_t thrown = append_handler<TB>(x.ref(), __ballot(1), r + 1, lv, q.term, q.leader_id, pv,
                                                        q.prev_log_term, __ballot(q.has_entry != 0),
                                                        Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
                                                        cnt, rt, su);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
-            append_command<TB>(x.ref(), __ballot(1), lr, p.cap, ((const uint32_t*)req)[o], cnt);
+            append_command<TB>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);
         }
         resolve_rep_draw(x, p, t, gid, r);
     }
     store_rep(x, p, idx);
+    if (cnt.miss) atomicAdd(misses, cnt.miss);
+}
+
+// read_log / write_log: the host's [n][R][log_cap] image of groups [g0, g0+n)
+// <-> the slot-major ring; only the retained slots [max(0, physLen - W),
+// physLen) are copied (the rest reads as 0 and is never written).
+__global__ __launch_bounds__(BLOCK) void log_image_kernel(DevParams p, int64_t g0, int64_t n, uint2* img, int to_ring) {
+    const int64_t total = n * p.R * (int64_t)p.cap;
+    for (int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x; k < total; k += (int64_t)gridDim.x * BLOCK) {
+        const int64_t rr = k / p.cap;                                     // (group - g0) * R + r
+        const int32_t j = (int32_t)(k - rr * p.cap);
+        const int64_t idx = g0 * p.R + rr;
+        const int32_t phys = p.st[fidx(p, RAFT_F_PHYS, idx)];
+        const bool in = j >= window_lo(p, phys) && j < phys;
+        uint2* slot = log_of(p, idx).at(j);
+        if (to_ring) {
+            if (in) *slot = img[k];
+        } else {
+            img[k] = in ? *slot : make_uint2(0u, 0u);
+        }
+    }
 }
 
 }  // namespace
@@ -600,8 +643,8 @@ template <int R> struct LogMatchL {
     }
 };
 template <int R> struct DigestL {
-    static void run(raft_engine* e, unsigned long long* out) {
-        digest_kernel<R><<<(unsigned)((e->p.G + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, out);
+    static void run(raft_engine* e, int64_t g0, int64_t n, unsigned long long* out) {
+        digest_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, g0, n, out);
     }
 };
 
@@ -655,6 +698,9 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_EINVAL, "bad timer constants");
     if (p->mode != RAFT_MODE_REFERENCE && p->mode != RAFT_MODE_TEXTBOOK)
         return fail(RAFT_EINVAL, "mode must be RAFT_MODE_REFERENCE or RAFT_MODE_TEXTBOOK");
+    if (p->log_window < 0 || (p->log_window & (p->log_window - 1)) || p->log_window > p->log_cap)
+        return fail(RAFT_EINVAL, "log_window must be 0 or a power of two <= log_cap");
+    if (p->G * p->R >= (int64_t)0x100000000ll) return fail(RAFT_EINVAL, "G * R must be < 2^32");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RAFT_ENODEV, "no HIP device");
     if (device < 0 || device >= ndev) return fail(RAFT_EINVAL, "bad device index");
@@ -671,6 +717,11 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const int64_t G = p->G, R = p->R;
     DevParams& d = e->dp;
     d.G = G; d.g0 = p->g0; d.R = p->R; d.cap = p->log_cap;
+    // the ring: log_window slots per replica (mask j & (W - 1)), or every
+    // physical slot (no wrap: j < log_cap, and no access is ever a miss)
+    const int64_t nslots = p->log_window ? p->log_window : p->log_cap;
+    d.wmask = p->log_window ? (uint32_t)(p->log_window - 1) : 0xFFFFFFFFu;
+    d.W = p->log_window ? p->log_window : (1 << 30);
     d.key0 = (uint32_t)p->seed; d.key1 = (uint32_t)(p->seed >> 32);
     d.P = p->heartbeat_ms; d.emin = p->election_min_ms; d.emax = p->election_max_ms;
     d.bmin = p->backoff_min_ms; d.bmax = p->backoff_max_ms; d.round_to = p->round_timeout_ms; d.retry = p->retry_ms;
@@ -687,7 +738,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t ses_b = (size_t)2 * R * G * 4;
     const size_t spill_b = (size_t)2 * R * R * G * 4;
     const size_t gx_b = (size_t)GX_WORDS * G * 4;
-    const size_t log_b = (size_t)G * R * p->log_cap * 8;
+    const size_t log_b = (size_t)G * R * nslots * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     // sized for the largest launch, so steps_per_launch can change later
     const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;
@@ -890,6 +941,25 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
     return RAFT_OK;
 }
 
+// the [n][R][log_cap] host image of groups [g0, g0+n) through a device buffer
+static int log_image(raft_engine* e, int64_t g0, int64_t n, std::vector<uint2>& tmp, bool to_ring) {
+    const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
+    uint2* buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, cnt * 8));
+    hipError_t err = hipSuccess;
+    if (to_ring) err = hipMemcpyAsync(buf, tmp.data(), cnt * 8, hipMemcpyHostToDevice, e->stream);
+    if (err == hipSuccess) {
+        const unsigned grid = (unsigned)std::min<size_t>((cnt + BLOCK - 1) / BLOCK, 65536);
+        log_image_kernel<<<grid, BLOCK, 0, e->stream>>>(e->dp, g0, n, buf, to_ring ? 1 : 0);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess && !to_ring) err = hipMemcpyAsync(tmp.data(), buf, cnt * 8, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    (void)hipFree(buf);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
 int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds) {
     if (int rc = check_range(e, g0, n)) return rc;
     if (n == 0) return RAFT_OK;
@@ -897,9 +967,7 @@ int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, 
     HIP_TRY(hipSetDevice(e->device));
     const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
     std::vector<uint2> tmp(cnt);
-    HIP_TRY(hipMemcpyAsync(tmp.data(), e->dp.log + (size_t)g0 * e->p.R * e->p.log_cap, cnt * 8,
-                           hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int rc = log_image(e, g0, n, tmp, false)) return rc;
     for (size_t k = 0; k < cnt; ++k) { terms[k] = (int32_t)tmp[k].x; cmds[k] = tmp[k].y; }
     return RAFT_OK;
 }
@@ -913,20 +981,25 @@ int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* 
     std::vector<uint2> tmp(cnt);
     for (size_t k = 0; k < cnt; ++k) tmp[k] = make_uint2((uint32_t)terms[k], cmds[k]);
     e->cache_valid = false;
-    HIP_TRY(hipMemcpyAsync(e->dp.log + (size_t)g0 * e->p.R * e->p.log_cap, tmp.data(), cnt * 8,
-                           hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    return RAFT_OK;
+    return log_image(e, g0, n, tmp, true);
 }
 
 int raft_engine_digest(raft_engine* e, uint64_t* out) {
-    if (!e || !out) return fail(RAFT_EINVAL, "null argument");
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    return raft_engine_digest_range(e, 0, e->p.G, out);
+}
+
+int raft_engine_digest_range(raft_engine* e, int64_t g0, int64_t n, uint64_t* out) {
+    if (int rc = check_range(e, g0, n)) return rc;
+    if (!out) return fail(RAFT_EINVAL, "null argument");
+    *out = 0;
+    if (n == 0) return RAFT_OK;
     HIP_TRY(hipSetDevice(e->device));
     unsigned long long* d = nullptr;
     HIP_TRY(hipMalloc(&d, 8));
     hipError_t err = hipMemsetAsync(d, 0, 8, e->stream);
     if (err == hipSuccess) {
-        dispatch_R<DigestL>(e->p.R, e, d);
+        dispatch_R<DigestL>(e->p.R, e, g0, n, d);
         err = hipMemcpyAsync(out, d, 8, hipMemcpyDeviceToHost, e->stream);
     }
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
@@ -988,7 +1061,10 @@ static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32
     char* buf = nullptr;
     HIP_TRY(hipMalloc(&buf, b_keys + b_off + b_ord + b_req + b_resp + 64));
     char* pk = buf; char* po = pk + b_keys; char* pd = po + b_off; char* pq = pd + b_ord; char* ps = pq + b_req;
-    hipError_t err = hipMemcpyAsync(pk, keys.data(), b_keys, hipMemcpyHostToDevice, e->stream);
+    unsigned int* pm = (unsigned int*)(ps + ((b_resp + 7) & ~(size_t)7));      // window-miss count
+    unsigned int misses = 0;
+    hipError_t err = hipMemsetAsync(pm, 0, 4, e->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(pk, keys.data(), b_keys, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(po, off.data(), b_off, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(pd, order.data(), b_ord, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(pq, req, b_req, hipMemcpyHostToDevice, e->stream);
@@ -996,13 +1072,17 @@ static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32
         auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true> : batch_kernel<false>;
         kern<<<(nk + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
             e->dp, (uint32_t)e->t, kind, nk, (const int64_t*)pk, (const int64_t*)po, (const int64_t*)pd, pq,
-            resp_sz ? (void*)ps : nullptr);
+            resp_sz ? (void*)ps : nullptr, pm);
         err = hipGetLastError();
     }
     if (err == hipSuccess && resp_sz) err = hipMemcpyAsync(resp, ps, b_resp, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(&misses, pm, 4, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     (void)hipFree(buf);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    if (misses)
+        return fail(RAFT_EWINDOW, std::to_string(misses) + " log accesses below the retained log_window: "
+                                  "the batch's results are not the reference's");
     return RAFT_OK;
 }
 

@@ -69,7 +69,9 @@ constexpr int GX_ISO = 0, GX_CMDS = 1, GX_S0 = 2, GX_WORDS = 3;
 //   ses   int32 [2][G*R]            primary session of group g: nextIndex / matchIndex towards replica r
 //   spill int32 [2][G*R][R]         every other session row: [(g*R + d) * R + s]
 //   gx    int32 [GX_WORDS][G]       isolation word, commands issued, primary-session owner s0 (-1 none)
-//   log   uint2 [G*R][cap]          (term, cmd) physical slots
+//   log   uint2 [NW][G*R]           (term, cmd) physical slots, slot-major: physical index j of
+//                                   replica idx at [(j & wmask) * G*R + idx]; NW = log_window (a
+//                                   ring of the newest NW slots) or log_cap (every slot, wmask ~0)
 struct DevParams {
     int32_t* st;
     int32_t* ses;
@@ -78,6 +80,8 @@ struct DevParams {
     uint2* log;
     int64_t G, g0, GR;
     int32_t R, cap;
+    uint32_t wmask;                            // slot of physical index j: j & wmask
+    int32_t W;                                 // window: accesses below physLen - W are misses (2^30 if none)
     uint32_t key0, key1;
     int32_t P, emin, emax, bmin, bmax, round_to, retry;
     uint32_t drop_ppm, drop_thr16;             // hit16(u) == (u < drop_thr16)
@@ -87,6 +91,21 @@ struct DevParams {
 };
 
 struct Entry { int32_t term; uint32_t cmd; };
+
+// One replica's log in HBM (the reference's ArrayList, Commons.kt:51): the
+// slot-major ring of DevParams::log seen from that replica.  Same-slot
+// entries of neighbouring replicas are adjacent, so the replicas of a group
+// appending the same index in one step write one contiguous run.
+struct LogView {
+    uint2* base;              // slot 0 of this replica: log + idx
+    uint32_t wmask, gr;       // slot mask; G*R (< 2^32), the stride between slots
+    int32_t cap, W;
+    __device__ __forceinline__ uint2* at(int32_t j) const { return base + (uint64_t)((uint32_t)j & wmask) * gr; }
+    // the view of the replica `d` lanes (replica indices) away in the same group
+    __device__ __forceinline__ LogView lane(int d) const { return LogView{base + d, wmask, gr, cap, W}; }
+    // a reference access of physical index j is below the retained window
+    __device__ __forceinline__ uint64_t miss(int32_t j, int32_t phys) const { return __ballot(j < phys - W); }
+};
 
 // The step kernel's DevParams as seen through the kernarg segment (constant
 // address space, so every field read is one scalar load).  Rarely used
@@ -209,14 +228,19 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
 //
 // TB (RAFT_MODE_TEXTBOOK): an array log instead -- slot i is written and
 // everything after it dropped (no ghost tail); physLen is the high-water mark.
+//
+// miss: the lanes whose write is a reference access below the window (the
+// overwrite branch, or any textbook write, at i < physLen - W); an append at
+// physLen never is.
 template <bool TB = false>
-__device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
-                                        uint64_t& overflow) {
+__device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
+                                        uint64_t& overflow, uint64_t& miss) {
     const int32_t last = n.last, phys = n.phys;
     const uint64_t app = lm(i == last);
     const uint64_t ghost = TB ? 0ull : app & lm(phys != last);   // the stale slot log[last] becomes the last entry
-    overflow = TB ? act & lm(i >= cap) : act & app & lm(phys >= cap);
+    overflow = TB ? act & lm(i >= lv.cap) : act & app & lm(phys >= lv.cap);
     wrote = act & ~overflow;
+    miss = (TB ? wrote : wrote & ~app) & lv.miss(i, phys);
     // the one slot the new tail cache needs from HBM
     const uint64_t ld = wrote & (ghost | (lm(i != last) & lm(i >= 1) & lm(i != last - 1)));
     const bool ap = ib(app);
@@ -229,14 +253,14 @@ __device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, En
     // also counts its earlier log stores) only when a load was issued
     if (ld) {
         if (ib(ld)) {
-            const uint2 g = lr[ap ? last : i - 1];
+            const uint2 g = *lv.at(ap ? last : i - 1);
             t1 = ap ? (int32_t)g.x : t1;                    // ghost: log[last] is the new last entry
             c1 = ap ? g.y : c1;
             t2 = ap ? t2 : (int32_t)g.x;                    // overwrite: log[i-1] becomes second-to-last
         }
     }
     const bool w = ib(wrote);
-    if (w) lr[(ap && !TB) ? phys : i] = make_uint2((uint32_t)e.term, e.cmd);
+    if (w) *lv.at((ap && !TB) ? phys : i) = make_uint2((uint32_t)e.term, e.cmd);
     n.t1 = w ? t1 : n.t1;
     n.c1 = w ? c1 : n.c1;
     n.t2 = w ? t2 : n.t2;
@@ -248,7 +272,7 @@ __device__ __forceinline__ void log_add(uint2* lr, int cap, Rep n, int32_t i, En
 // ---- vote() (RaftServer.kt:228-251), applied on the lanes of act ----------
 template <bool TB, class CNT>
 __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, int32_t rt, int32_t rc, int32_t rli,
-                                             int32_t rlt, CNT& cnt, int32_t& resp_term, uint64_t& granted) {
+                                             int32_t rlt, int32_t W, CNT& cnt, int32_t& resp_term, uint64_t& granted) {
     if constexpr (TB) {
         // textbook: a higher term is adopted whatever the answer (Q5 adopts it
         // only on a grant); grant iff votedFor is free or the candidate and the
@@ -264,6 +288,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
         const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));
         granted = elig & ~logrej;
         cnt.add(elig & hasl, RAFT_C_VOTE_LOG_READS);
+        cnt.add(elig & hasl & lm(n.last - 1 < n.phys - W), RAFT_C_LOG_WINDOW_MISS);   // log.get(lastIndex - 1)
         cnt.add(granted, RAFT_C_VOTES_GRANTED);
         n.voted = ib(granted) ? rc : n.voted;
         n.fl |= ib(granted & lm(rc != id)) ? follower_sent(n.fl) : 0u;
@@ -276,6 +301,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
     const uint64_t up = act & higher & ~logrej;                                 // :237-242
     granted = up | (act & lm(rt == n.term) & lm(n.voted == rc));                // :230
     cnt.add(act & higher & hasl, RAFT_C_VOTE_LOG_READS);
+    cnt.add(act & higher & hasl & lm(n.last - 1 < n.phys - W), RAFT_C_LOG_WINDOW_MISS);   // :233 log.get
     cnt.add(granted, RAFT_C_VOTES_GRANTED);
     const bool u = ib(up);
     n.fl |= u ? follower_sent(n.fl) : 0u;                                       // :241
@@ -297,7 +323,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
 // commit follows leaderCommit only after the consistency check, up to the last
 // entry the request vouches for, and never goes down.
 template <bool TB, class CNT>
-__device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, uint2* lr, int cap, int32_t rt,
+__device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, const LogView& lv, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
                                                    Entry e, int32_t lcommit, int32_t dprev, int32_t dnext, CNT& cnt,
                                                    int32_t& resp_term, uint64_t& success) {
@@ -318,13 +344,20 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
     const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
     const uint64_t thrown = check & lm(prev < 0);
     cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
+    uint64_t miss = act & check & ~thrown & lv.miss(prev, n.phys);              // :276 log.get(prevLogIndex)
     success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
-    uint64_t wrote, ovf;
+    uint64_t wrote, ovf, wmiss;
     uint64_t same = 0;                                                          // TB: entry already there
-    if constexpr (TB) same = success & has & lm(prev + 1 < n.last) & lm(dnext == e.term);
-    log_add<TB>(lr, cap, n, prev + 1, e, success & has & ~same, wrote, ovf);    // :278 (Q2, Q10)
+    if constexpr (TB) {
+        const uint64_t rd = success & has & lm(prev + 1 < n.last);              // TB: reads log[prev + 1]
+        miss |= rd & lv.miss(prev + 1, n.phys);
+        same = rd & lm(dnext == e.term);
+    }
+    log_add<TB>(lv, n, prev + 1, e, success & has & ~same, wrote, ovf, wmiss);  // :278 (Q2, Q10)
     cnt.add(wrote, RAFT_C_ENTRY_WRITES);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
+    cnt.add(miss, RAFT_C_LOG_WINDOW_MISS);
+    cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);
     if constexpr (TB) {
         const int32_t lastNew = prev + 1 + (ib(wrote | same) ? 1 : 0);
         const int32_t cc = max(n.commit, min(lcommit, lastNew));
@@ -336,11 +369,12 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
 
 // ---- appendCommand() (RaftServer.kt:100-107), applied on the lanes of act -
 template <bool TB, class CNT>
-__device__ __forceinline__ void append_command(Rep n, uint64_t act, uint2* lr, int cap, uint32_t cmd, CNT& cnt) {
-    uint64_t wrote, ovf;
-    log_add<TB>(lr, cap, n, n.last, Entry{n.term, cmd}, act, wrote, ovf);
+__device__ __forceinline__ void append_command(Rep n, uint64_t act, const LogView& lv, uint32_t cmd, CNT& cnt) {
+    uint64_t wrote, ovf, wmiss;
+    log_add<TB>(lv, n, n.last, Entry{n.term, cmd}, act, wrote, ovf, wmiss);
     cnt.add(act, RAFT_C_COMMANDS);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
+    cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                                     // TB only: add(lastIndex) writes slot last
 }
 
 // ---------------------------------------------------------------------------
@@ -408,7 +442,7 @@ struct Ctx {
     bool live;                // lane holds a real replica (whole groups are live or not)
     int iso;                  // isolated replica this step, -1 if none
     uint32_t part;            // replicas on side B of this step's partition
-    uint2* lr;                // this replica's log
+    uint2* lr;                // this replica's log: slot 0 (DevParams::log + g * R + r)
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
     uint32_t* jl;             // the wave's LDS staging of the job words, [64 lanes][4]
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
@@ -425,6 +459,12 @@ struct Ctx {
     }
     __device__ __forceinline__ uint32_t gid() const { return gg0 + j(); }          // global group id
     __device__ __forceinline__ int64_t idx() const { return (int64_t)wg0 * R + base + r; }   // g * R + r
+    // the ring's geometry is re-read from the kernarg segment where it is used
+    // (kept live across the step loop it would pin SGPRs, see kernargs())
+    __device__ __forceinline__ LogView log(const DevParams&) const {
+        const KernArgs kp = kernargs();
+        return LogView{lr, kp->wmask, (uint32_t)kp->GR, kp->cap, kp->W};
+    }
 };
 
 // The lanes whose message s -> d is lost (S-7): churn isolation, partition
@@ -576,6 +616,7 @@ struct Stepper {
         const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
         const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
         const uint32_t Lc1 = bcastu(n.c1, sl);
+        const int32_t Llo = bcast(n.phys, sl) - kernargs()->W;          // the leader's window floor
         const uint64_t mtk = lm(tk), mme = lm(c.r == s);
         const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
         uint32_t dw;
@@ -601,6 +642,8 @@ struct Stepper {
         const uint64_t has = pge & lm(i <= Llast);
         cnt.add(run & p0 & plt, RAFT_C_PREV_READS_LEADER);
         cnt.add(run & has, RAFT_C_ENTRY_READS_LEADER);
+        cnt.add(run & p0 & plt & lm(prev < Llo), RAFT_C_LOG_WINDOW_MISS);      // :128 log.get(prevLogIndex)
+        cnt.add(run & has & lm(i - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);         // :131 log.get(i - 1)
         // RAFT_C_APPEND_SKIPPED (run & ~ok) is not counted here: run covers
         // whole groups, so it is R * SESSIONS_TICKED - APPEND_SENT, which the
         // counter reduction derives (reduce_counters_kernel)
@@ -611,7 +654,8 @@ struct Stepper {
         // tick can change a slot another one reads.  The tail caches answer
         // all but: leader log[prev] below its last two slots, an entry other
         // than the leader's newest, own log[prev] below the last two slots.
-        const uint2* ls = c.lr + (int64_t)(s - c.r) * p.cap;
+        const LogView lv = c.log(p);
+        const LogView ls = lv.lane(s - c.r);                              // the leader's log
         int32_t lpt = cached_term(Llast, Lt1, Lt2, prev);
         int32_t dpt = cached_term(n.last, n.t1, n.t2, prev);
         int32_t dnt = TB ? cached_term(n.last, n.t1, n.t2, prev + 1) : 0;  // TB: own log[prev+1]
@@ -621,10 +665,10 @@ struct Stepper {
         const uint64_t ld3 = ok & p0 & lm(prev < n.last - 2);
         const uint64_t ld4 = TB ? ok & has & lm(prev + 1 < n.last - 2) : 0ull;
         if (ld1 | ld2 | ld3 | ld4) {                                      // rare: tail-cache misses
-            if (ib(ld1)) lpt = (int32_t)ls[prev].x;
-            if (ib(ld2)) lent = ls[i - 1];
-            if (ib(ld3)) dpt = (int32_t)c.lr[prev].x;
-            if (TB && ib(ld4)) dnt = (int32_t)c.lr[prev + 1].x;
+            if (ib(ld1)) lpt = (int32_t)ls.at(prev)->x;
+            if (ib(ld2)) lent = *ls.at(i - 1);
+            if (ib(ld3)) dpt = (int32_t)lv.at(prev)->x;
+            if (TB && ib(ld4)) dnt = (int32_t)lv.at(prev + 1)->x;
             asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt), "v"(dnt));   // wait inside the branch
         }
 
@@ -637,7 +681,7 @@ struct Stepper {
         int32_t rterm;
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
-        append_handler<TB>(n.rep(), act, c.r + 1, c.lr, p.cap, Lterm, s + 1, prev, lpt, has,
+        append_handler<TB>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
                            Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
@@ -709,8 +753,9 @@ struct Stepper {
                 const uint64_t cand = run & lm(!stepdown) & lm(N > C) & lm(N <= Llast);
                 int32_t NT = N - 1 == Llast - 1 ? Lt1 : Lt2;
                 const uint64_t ldn = cand & lm(N - 1 < Llast - 2);
+                cnt.add(cand & lm(N - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);
                 if (ldn) {
-                    if (ib(ldn)) NT = (int32_t)ls[N - 1].x;
+                    if (ib(ldn)) NT = (int32_t)ls.at(N - 1)->x;
                     asm volatile("" :: "v"(NT));
                 }
                 const uint64_t adv = cand & lm(NT == Lterm);
@@ -764,7 +809,7 @@ struct Stepper {
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
-        vote_handler<TB>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, cnt, rterm, granted);
+        vote_handler<TB>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, kernargs()->W, cnt, rterm, granted);
         const uint64_t lresp = act & lost(p, c, s, r, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
@@ -850,6 +895,7 @@ struct Stepper {
             qli = n.last;
             qlt = n.last != 0 ? n.t1 : 0;
             cnt.add((sr | resend) & lm(n.last != 0), RAFT_C_VOTE_LOG_READS);
+            cnt.add((sr | resend) & lm(n.last != 0) & lm(n.last - 1 < n.phys - kernargs()->W), RAFT_C_LOG_WINDOW_MISS);
             cnt.add(sr, RAFT_C_ROUNDS);
         }
         start_sessions(p, c, n, sstart, cnt);
@@ -1017,7 +1063,7 @@ struct Stepper {
             const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
                                 lm(lead != 0);
             const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
-            append_command<TB>(n.rep(), tgt, c.lr, p.cap, hw2, cnt);
+            append_command<TB>(n.rep(), tgt, c.log(p), hw2, cnt);
             n.cmdc = inc_if(n.cmdc, cm);
         }
 

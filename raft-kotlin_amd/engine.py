@@ -142,6 +142,12 @@ class RaftEngine:
         self._check(self._lib.raft_engine_digest(self._h, C.byref(out)), "digest")
         return int(out.value)
 
+    def digest_range(self, g0: int, n: int) -> int:
+        """The digest of groups [g0, g0 + n) only."""
+        out = C.c_uint64()
+        self._check(self._lib.raft_engine_digest_range(self._h, g0, n, C.byref(out)), "digest_range")
+        return int(out.value)
+
     def check_log_matching(self, g0: int = 0, n: int | None = None, flags: bool = False):
         """Groups whose replicas disagree inside their common committed prefix
         (safety flag, include/raft_engine.h); returns the count, or (count,

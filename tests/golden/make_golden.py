@@ -27,6 +27,11 @@ CASES = {
     "c3s": dict(steps=400, digest_every=1, log_cap=160,
                 **dict(abi.CONFIGS[3], G=64, churn_ppm=20_000)),
     "c5s": dict(steps=400, digest_every=1, log_cap=600, **dict(abi.CONFIGS[5], G=32)),
+    # the ring-buffered log (log_window): config 2 wraps a
+    # 4-slot ring ~20 times, config 3 a 64-slot one; neither misses
+    "c2w": dict(steps=300, digest_every=1, log_cap=128, log_window=4, **dict(abi.CONFIGS[2], G=64)),
+    "c3w": dict(steps=400, digest_every=1, log_cap=160, log_window=64,
+                **dict(abi.CONFIGS[3], G=64, churn_ppm=20_000)),
 }
 
 
@@ -40,7 +45,9 @@ def run_case(spec):
         digests.append(o.digest())
     st = o.read_state()
     t, c = masked_logs(st, *o.read_log(), o.R)
-    return np.concatenate(counters), digests, st, t, c
+    counters = np.concatenate(counters)
+    assert counters[:, abi.C_INDEX["log_window_miss"]].sum() == 0
+    return counters, digests, st, t, c
 
 
 def main():

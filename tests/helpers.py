@@ -70,15 +70,17 @@ def assert_same_logs(a_state, a_logs, b_logs, R, label=""):
         raise AssertionError(f"{label}: {len(bad)} log slots differ; first {bad[0].tolist()}")
 
 
-def log_matching_flags(state: np.ndarray, terms: np.ndarray, cmds: np.ndarray, R: int) -> np.ndarray:
+def log_matching_flags(state: np.ndarray, terms: np.ndarray, cmds: np.ndarray, R: int, window: int = 0) -> np.ndarray:
     """Per group: 1 if two replicas differ at an index inside both committed
-    prefixes (i < min(commitIndex, lastIndex) of each) -- the restatement of
+    prefixes (i < min(commitIndex, lastIndex) of each) and, with a log_window
+    W, inside both retained windows (i >= physLen - W) -- the restatement of
     raft_engine_check_log_matching used to check the kernel."""
     n, cap = terms.shape[0], terms.shape[2]
     c = np.stack([np.minimum(fld(state, R, r, "commit"), fld(state, R, r, "last")) for r in range(R)], -1)
     c = np.clip(c, 0, cap)                                        # [n, R]
+    lo = np.stack([fld(state, R, r, "phys") - window if window else np.zeros(n, np.int64) for r in range(R)], -1)
     idx = np.arange(cap)
-    cover = idx[None, None, :] < c[:, :, None]                    # [n, R, cap]
+    cover = (idx[None, None, :] < c[:, :, None]) & (idx[None, None, :] >= lo[:, :, None])   # [n, R, cap]
     bad = np.zeros(n, dtype=bool)
     for a in range(R):
         for b in range(a + 1, R):

@@ -42,9 +42,9 @@ def fl(*bits, pending=0, votes=0, latch=0):
     return v | (pending << 8) | (votes << 16) | (latch << 20)
 
 
-def params(R, G=1):
-    return dict(R=R, G=G, log_cap=64, seed=77, election_min_ms=20000, election_max_ms=20000,
-                backoff_min_ms=2000, backoff_max_ms=2000)
+def params(kat, G=1):
+    return dict(R=kat["R"], G=G, log_cap=64, seed=77, election_min_ms=20000, election_max_ms=20000,
+                backoff_min_ms=2000, backoff_max_ms=2000, log_window=kat.get("window", 0))
 
 
 def node(w, R, r, **kv):
@@ -261,7 +261,31 @@ K14 = dict(name="K14 FOLLOWER send deferred during an election", R=3, setup=k14_
      {}, dict(votes_granted=0, rounds=0, timeouts=0, sessions_ticked=1)),
 ])
 
-KATS = [K8, K9, K10, K11, K12, K13, K14]
+# ---------------------------------------------------------------------------
+# K15 the ring's window misses (raft_params.log_window).  R=3,
+#     a 4-slot ring.  Every replica holds lastIndex 2 over a physical list of
+#     8 (a ghost tail: 6 slots beyond lastIndex), so the retained slots are
+#     [4, 8).  Leader 0's session has nextIndex 3 towards everyone: each of
+#     the 3 requests does log.get(prevLogIndex = 1) (:128) -- 1 < 8 - 4, a
+#     miss -- and carries no entry (lastIndex 2 < 3, :130); each destination's
+#     append() does log.get(1) again (:276), another miss.  6 misses, and
+#     the run is marked invalid (the values read are NOT the reference's: the
+#     slots were overwritten by the ring, so no state is checked beyond it).
+# ---------------------------------------------------------------------------
+def k15_setup(w, R):
+    node(w, R, 0, role=L, term=1, voted=1, flags=HB, last=2, phys=8)
+    for r in (1, 2):
+        node(w, R, r, term=1, voted=1, flags=ARMED, election_ms=FAR, last=2, phys=8)
+    set_session(w, R, 0, [3, 3, 3], [0, 0, 0])
+
+
+K15 = dict(name="K15 ring window misses are counted", R=3, window=4, setup=k15_setup,
+           logs={r: [(1, 10 + j) for j in range(8)] for r in range(3)}, checks=[
+    (1, {}, {}, dict(sessions_ticked=1, append_sent=3, prev_reads_leader=3, prev_reads_follower=3,
+                     entry_reads_leader=0, log_window_miss=6)),
+])
+
+KATS = [K8, K9, K10, K11, K12, K13, K14, K15]
 
 
 def initial(kat):

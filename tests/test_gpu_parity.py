@@ -57,7 +57,7 @@ def check_log_matching(e, o, label):
     """The kernel's Log Matching flags vs the numpy restatement on the oracle's logs."""
     so = o.read_state()
     t, c = o.read_log()
-    want = log_matching_flags(so, t, c, e.R)
+    want = log_matching_flags(so, t, c, e.R, int(e.p.log_window))
     n, got = e.check_log_matching(flags=True)
     assert np.array_equal(got, want), f"{label}: log-matching flags differ in {np.count_nonzero(got != want)} groups"
     assert n == int(want.sum())
@@ -122,12 +122,15 @@ def test_config2_parity_every_step():
     run_lockstep(e, o, abi.CONFIG_STEPS[2], 10, "config2", digest_every=1)
 
 
-def test_config3_drops_churn_reduced():
-    """BASELINE config 3 semantics (5% drop + leader-isolation churn) at reduced G/steps."""
+@pytest.mark.parametrize("window", [0, 64])
+def test_config3_drops_churn_reduced(window):
+    """BASELINE config 3 semantics (5% drop + leader-isolation churn) at reduced
+    G/steps, with every physical slot kept and on a 64-slot ring (the logs
+    wrap ~10 times; no access misses it)."""
     kw = dict(abi.CONFIGS[3])
     kw.update(G=20_000, churn_ppm=5_000)
-    e, o = pair(log_cap=768, **kw)
-    se, ov = run_lockstep(e, o, 2_000, 100, "config3", digest_every=5)
+    e, o = pair(log_cap=768, log_window=window, **kw)
+    se, ov = run_lockstep(e, o, 2_000, 100, f"config3 W={window}", digest_every=5)
     assert ov == 0
     check_log_matching(e, o, "config3")
 
@@ -207,11 +210,14 @@ def test_full_size_config3_sampled():
 
 # ---- RAFT_MODE_TEXTBOOK (opt-in, not the reference) ------------
 
-@pytest.mark.parametrize("cfg", [2, 3, 5])
+@pytest.mark.parametrize("cfg", [2, 3, 5, "3w"])
 def test_textbook_lockstep(cfg):
     """The textbook kernel (step_kernel<R, true>) against the oracle's textbook
-    mode, bit-exact, and its committed prefixes Log-Matching clean."""
-    kw = dict(abi.CONFIGS[cfg], mode=abi.MODE_TEXTBOOK)
+    mode, bit-exact, and its committed prefixes Log-Matching clean ("3w": on a
+    64-slot ring)."""
+    win = 64 if cfg == "3w" else 0
+    cfg = 3 if cfg == "3w" else cfg
+    kw = dict(abi.CONFIGS[cfg], mode=abi.MODE_TEXTBOOK, log_window=win)
     kw.update({2: dict(G=5_000), 3: dict(G=10_000, churn_ppm=10_000), 5: dict(G=1_000)}[cfg])
     steps, cap = {2: (400, 200), 3: (1_200, 500), 5: (1_200, 1_400)}[cfg]
     e, o = pair(log_cap=cap, steps_per_launch=32, **kw)
@@ -246,7 +252,8 @@ def test_full_size_digest(cfg, spl):
     want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))[f"c{cfg}_counters"]
     kw = dict(abi.CONFIGS[cfg])
     assert meta["groups"] == kw["G"] and meta["params"] == {k: v for k, v in kw.items() if k != "G"}
-    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], steps_per_launch=spl, **kw))
+    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], log_window=meta["log_window"], steps_per_launch=spl,
+                                   **kw))
     ce = e.step(meta["steps"])
     if not np.array_equal(ce, want):
         bad = np.argwhere(ce != want)[0]
@@ -254,7 +261,45 @@ def test_full_size_digest(cfg, spl):
                              f"{ce[tuple(bad)]} vs {want[tuple(bad)]}")
     assert f"{e.digest():016x}" == meta["digest"], f"config {cfg}: whole-run digest differs"
     assert ce[:, abi.C_INDEX["log_overflow"]].sum() == 0
+    assert ce[:, abi.C_INDEX["log_window_miss"]].sum() == 0
     e.close()
+
+
+def test_full_size_config3_1e5_steps_on_the_ring():
+    """config 3 at 10^6 x 5 for 10^5 steps on the bench's 256-slot ring
+    (log_window): 10 GB of log where a flat log would need 1.2 TB.  No access
+    misses the window and no log overflows (whole engine); groups [0, 10^4)
+    equal the oracle's digest (tests/golden/make_full_size.py, "c3long")."""
+    import json
+    meta = json.load(open(FULL))["c3long"]
+    kw = dict(abi.CONFIGS[3])
+    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], log_window=meta["log_window"],
+                                   steps_per_launch=500, **kw))
+    assert e.device_bytes < 16 * 2 ** 30
+    ce = e.step(meta["steps"])
+    assert ce[:, abi.C_INDEX["log_overflow"]].sum() == 0
+    assert ce[:, abi.C_INDEX["log_window_miss"]].sum() == 0
+    assert f"{e.digest_range(0, meta['sample_groups']):016x}" == meta["digest"]
+    assert ce[-1, abi.C_INDEX["groups_with_leader"]] > 0.9 * kw["G"]
+    e.close()
+
+
+def test_window_misses_are_counted():
+    """A ring too small for the run (16 slots under 10 % drops and partitions):
+    the engine counts its first misses in the same step as the oracle, and
+    every step before it is bit-identical (the run is invalid from there on)."""
+    kw = dict(R=5, G=3000, seed=105, log_cap=300, drop_ppm=100_000, churn_ppm=20_000, churn_steps=15,
+              cmd_ppm=500_000, partition_period=40, partition_len=10, log_window=16)
+    e, o = pair(**kw)
+    mi = abi.C_INDEX["log_window_miss"]
+    for t in range(200):
+        ce, co = e.step(1), o.step(1)[:, : abi.NUM_COUNTERS]
+        if co[0, mi]:
+            assert ce[0, mi] > 0, f"step {t}: the oracle counts {co[0, mi]} misses, the engine none"
+            return
+        assert np.array_equal(ce, co), f"step {t}"
+        assert e.digest() == o.digest(), f"step {t}"
+    raise AssertionError("no miss in 200 steps")
 
 
 # ---- the service boundary: single handlers vs the oracle -------------------------
@@ -464,3 +509,20 @@ def test_node_entries_term_command_dump():
             want = [f"{int(ot[g, r, j])}: {svc2.commands.name(oc[g, r, j])}" for j in range(last)]
             assert svc2.node(g, r).entries() == want, (g, r)
             assert last == 0 or want[0].startswith(f"{int(ot[g, r, 0])}: cmd#")
+
+
+# ---- K8-K14 replayed through the engine (tests/kats_election.py) -----------------
+import kats_election as KE  # noqa: E402
+
+
+@pytest.mark.parametrize("kat", KE.KATS, ids=lambda k: k["name"].split()[0])
+def test_election_kats_on_engine(kat):
+    """The hand-derived election-loop traces through the C-ABI: write_state
+    (+ write_log), step, read_state; then the engine equals the oracle."""
+    kw = KE.params(kat)
+    e, o = pair(**kw)
+    KE.run(kat, e)
+    KE.run(kat, o)
+    if not kat.get("window"):                  # past a window miss the engine's values are not the reference's
+        assert_same_state(e.read_state(), o.read_state(), kat["R"], kat["name"])
+        assert e.digest() == o.digest()

@@ -194,5 +194,5 @@ import kats_election as KE  # noqa: E402
 
 @pytest.mark.parametrize("kat", KE.KATS, ids=lambda k: k["name"].split()[0])
 def test_election_kats_on_oracle(kat):
-    o = O.Oracle(abi.make_params(**KE.params(kat["R"])))
+    o = O.Oracle(abi.make_params(**KE.params(kat)))
     KE.run(kat, o)
