@@ -186,7 +186,6 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
     c.gg0 = (uint32_t)(p.g0 + c.wg0);
     const int64_t idx = g * R + r;
-    c.lr = p.log + (live ? idx : 0);
     c.iso = -1;
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
@@ -258,8 +257,14 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     }
 }
 
+// the log of replica idx = g * R + r outside the step kernel: lane
+// (g % GPW) * R + r of the block of step-kernel wave g / GPW
 __device__ __forceinline__ LogView log_of(const DevParams& p, int64_t idx) {
-    return LogView{p.log + idx, p.wmask, (uint32_t)p.GR, p.cap, p.W};
+    const int64_t g = idx / p.R;
+    const int gpw = 64 / p.R;
+    const int64_t w = g / gpw;
+    const int lane = (int)(g - w * gpw) * p.R + (int)(idx - g * p.R);
+    return LogView{p.log + ((w * p.nslots) << 6), (uint32_t)lane, p.wmask, p.cap, p.W};
 }
 // the retained physical slots of a replica: [max(0, physLen - W), physLen)
 __device__ __forceinline__ int32_t window_lo(const DevParams& p, int32_t phys) { return max(0, phys - p.W); }
@@ -700,7 +705,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_EINVAL, "mode must be RAFT_MODE_REFERENCE or RAFT_MODE_TEXTBOOK");
     if (p->log_window < 0 || (p->log_window & (p->log_window - 1)) || p->log_window > p->log_cap)
         return fail(RAFT_EINVAL, "log_window must be 0 or a power of two <= log_cap");
-    if (p->G * p->R >= (int64_t)0x100000000ll) return fail(RAFT_EINVAL, "G * R must be < 2^32");
+    if ((p->log_window ? p->log_window : p->log_cap) >= (1 << 23))
+        return fail(RAFT_EINVAL, "log slots per replica (log_window, else log_cap) must be < 2^23");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RAFT_ENODEV, "no HIP device");
     if (device < 0 || device >= ndev) return fail(RAFT_EINVAL, "bad device index");
@@ -722,6 +728,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const int64_t nslots = p->log_window ? p->log_window : p->log_cap;
     d.wmask = p->log_window ? (uint32_t)(p->log_window - 1) : 0xFFFFFFFFu;
     d.W = p->log_window ? p->log_window : (1 << 30);
+    d.nslots = (int32_t)nslots;
+    const int64_t log_waves = (G + 64 / R - 1) / (64 / R);           // step-kernel waves: one log block each
     d.key0 = (uint32_t)p->seed; d.key1 = (uint32_t)(p->seed >> 32);
     d.P = p->heartbeat_ms; d.emin = p->election_min_ms; d.emax = p->election_max_ms;
     d.bmin = p->backoff_min_ms; d.bmax = p->backoff_max_ms; d.round_to = p->round_timeout_ms; d.retry = p->retry_ms;
@@ -738,7 +746,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t ses_b = (size_t)2 * R * G * 4;
     const size_t spill_b = (size_t)2 * R * R * G * 4;
     const size_t gx_b = (size_t)GX_WORDS * G * 4;
-    const size_t log_b = (size_t)G * R * nslots * 8;
+    const size_t log_b = (size_t)log_waves * nslots * 64 * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     // sized for the largest launch, so steps_per_launch can change later
     const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;

@@ -69,9 +69,10 @@ constexpr int GX_ISO = 0, GX_CMDS = 1, GX_S0 = 2, GX_WORDS = 3;
 //   ses   int32 [2][G*R]            primary session of group g: nextIndex / matchIndex towards replica r
 //   spill int32 [2][G*R][R]         every other session row: [(g*R + d) * R + s]
 //   gx    int32 [GX_WORDS][G]       isolation word, commands issued, primary-session owner s0 (-1 none)
-//   log   uint2 [NW][G*R]           (term, cmd) physical slots, slot-major: physical index j of
-//                                   replica idx at [(j & wmask) * G*R + idx]; NW = log_window (a
-//                                   ring of the newest NW slots) or log_cap (every slot, wmask ~0)
+//   log   uint2 [waves][NW][64]     (term, cmd) physical slots, one contiguous block per step-kernel
+//                                   wave (GPW = 64 / R groups): physical index j of the replica in
+//                                   lane l of wave w at [w][j & wmask][l]; NW = log_window (a ring
+//                                   of the newest NW slots) or log_cap (every slot, no wrap)
 struct DevParams {
     int32_t* st;
     int32_t* ses;
@@ -82,6 +83,7 @@ struct DevParams {
     int32_t R, cap;
     uint32_t wmask;                            // slot of physical index j: j & wmask
     int32_t W;                                 // window: accesses below physLen - W are misses (2^30 if none)
+    int32_t nslots;                            // NW: slots per replica (< 2^23: 32-bit offsets in a block)
     uint32_t key0, key1;
     int32_t P, emin, emax, bmin, bmax, round_to, retry;
     uint32_t drop_ppm, drop_thr16;             // hit16(u) == (u < drop_thr16)
@@ -92,17 +94,23 @@ struct DevParams {
 
 struct Entry { int32_t term; uint32_t cmd; };
 
-// One replica's log in HBM (the reference's ArrayList, Commons.kt:51): the
-// slot-major ring of DevParams::log seen from that replica.  Same-slot
-// entries of neighbouring replicas are adjacent, so the replicas of a group
-// appending the same index in one step write one contiguous run.
+// One replica's log in HBM (the reference's ArrayList, Commons.kt:51): its
+// column of its wave's block [NW][64] of DevParams::log.  A wave's slots are
+// one contiguous region (few pages, whatever the slots its lanes touch), and
+// same-slot entries of a group's replicas are adjacent, so the replicas of a
+// group appending the same index in one step write one contiguous run.
 struct LogView {
-    uint2* base;              // slot 0 of this replica: log + idx
-    uint32_t wmask, gr;       // slot mask; G*R (< 2^32), the stride between slots
+    uint2* wbase;             // its wave's block (wave-uniform in the step kernel: an SGPR pair)
+    uint32_t col;             // its column: the replica's lane in that wave
+    uint32_t wmask;           // slot of physical index j: j & wmask (row stride 64 entries)
     int32_t cap, W;
-    __device__ __forceinline__ uint2* at(int32_t j) const { return base + (uint64_t)((uint32_t)j & wmask) * gr; }
+    // a 32-bit per-lane offset from a uniform base: global_load/store with saddr
+    __device__ __forceinline__ uint2* at(int32_t j) const {
+        const uint32_t off = (((uint32_t)j & wmask) << 9) | (col << 3);      // bytes: row * 512 + col * 8
+        return (uint2*)((char*)wbase + off);
+    }
     // the view of the replica `d` lanes (replica indices) away in the same group
-    __device__ __forceinline__ LogView lane(int d) const { return LogView{base + d, wmask, gr, cap, W}; }
+    __device__ __forceinline__ LogView lane(int d) const { return LogView{wbase, col + d, wmask, cap, W}; }
     // a reference access of physical index j is below the retained window
     __device__ __forceinline__ uint64_t miss(int32_t j, int32_t phys) const { return __ballot(j < phys - W); }
 };
@@ -442,7 +450,7 @@ struct Ctx {
     bool live;                // lane holds a real replica (whole groups are live or not)
     int iso;                  // isolated replica this step, -1 if none
     uint32_t part;            // replicas on side B of this step's partition
-    uint2* lr;                // this replica's log: slot 0 (DevParams::log + g * R + r)
+
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
     uint32_t* jl;             // the wave's LDS staging of the job words, [64 lanes][4]
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
@@ -459,11 +467,14 @@ struct Ctx {
     }
     __device__ __forceinline__ uint32_t gid() const { return gg0 + j(); }          // global group id
     __device__ __forceinline__ int64_t idx() const { return (int64_t)wg0 * R + base + r; }   // g * R + r
-    // the ring's geometry is re-read from the kernarg segment where it is used
-    // (kept live across the step loop it would pin SGPRs, see kernargs())
+    // This replica's log.  The wave's block and the ring's geometry are
+    // re-derived from the kernarg segment where they are used (kept live
+    // across the step loop they would pin SGPRs, see kernargs()).
     __device__ __forceinline__ LogView log(const DevParams&) const {
         const KernArgs kp = kernargs();
-        return LogView{lr, kp->wmask, (uint32_t)kp->GR, kp->cap, kp->W};
+        const uint32_t wave = wg0 / (uint32_t)Lanes<R>::GPW;                     // uniform
+        uint2* wb = kp->log + (((uint64_t)wave * (uint32_t)kp->nslots) << 6);
+        return LogView{wb, (uint32_t)(base + r), kp->wmask, kp->cap, kp->W};
     }
 };
 
