@@ -201,6 +201,8 @@ def load_library(path: str | None = None):
         "raft_wire_encode_append_resp": (I64, [P(raft_append_resp), I64, P(C.c_uint8), I64, P(I64)]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("RAFT_ENGINE_LIB") and not hasattr(lib, name):
+            continue                     # an older experimental build (RAFT_ENGINE_LIB) may lack newer entry points
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

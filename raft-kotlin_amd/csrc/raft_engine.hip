@@ -162,7 +162,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 #ifndef RAFT_STEP_WAVES_PER_EU
 #define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
 #endif
-template <int R, bool TB>
+template <int R, bool TB, bool RING>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
@@ -186,6 +186,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
     c.gg0 = (uint32_t)(p.g0 + c.wg0);
     const int64_t idx = g * R + r;
+    c.lr = p.log + ((int64_t)wid * 64 + lane) * p.nslots;               // its wave's block, its row
     c.iso = -1;
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
@@ -201,6 +202,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
     // previous step's log stores, so each step would start by waiting for them.
     __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
+    c.gapseen = RING && __ballot(live && n.phys - n.last >= p.W - 1) != 0;
     __syncthreads();                                                      // counter rows zeroed
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;
@@ -228,7 +230,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         }
         Counters cnt;
         cnt.clear();
-        Stepper<R, TB>::step(p, c, n, cnt);
+        Stepper<R, TB, RING>::step(p, c, n, cnt);
         c.clk.mark(PH_TDRAW);
 #ifdef RAFT_EXP_NO_FLUSH
 #pragma unroll
@@ -264,7 +266,7 @@ __device__ __forceinline__ LogView log_of(const DevParams& p, int64_t idx) {
     const int gpw = 64 / p.R;
     const int64_t w = g / gpw;
     const int lane = (int)(g - w * gpw) * p.R + (int)(idx - g * p.R);
-    return LogView{p.log + ((w * p.nslots) << 6), (uint32_t)lane, p.wmask, p.cap, p.W};
+    return LogView{p.log + (w * 64 + lane) * (int64_t)p.nslots, (uint32_t)p.nslots, p.wmask, p.cap, p.W};
 }
 // the retained physical slots of a replica: [max(0, physLen - W), physLen)
 __device__ __forceinline__ int32_t window_lo(const DevParams& p, int32_t phys) { return max(0, phys - p.W); }
@@ -531,8 +533,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
             uint64_t gr;
-            vote_handler<TB>(x.ref(), __ballot(1), r + 1, q.term, q.candidate_id, q.last_log_index, q.last_log_term,
-                             p.W, cnt, rt, gr);
+            vote_handler<TB, true>(x.ref(), __ballot(1), r + 1, q.term, q.candidate_id, q.last_log_index, q.last_log_term,
+                                   __ballot(x.phys - x.last >= p.W), cnt, rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
@@ -541,13 +543,13 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             const int32_t pv = q.prev_log_index;
             const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
             const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
-            const uint64_t thrown = append_handler<TB>(x.ref(), __ballot(1), r + 1, lv, q.term, q.leader_id, pv,
+            const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, q.term, q.leader_id, pv,
                                                        q.prev_log_term, __ballot(q.has_entry != 0),
                                                        Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
                                                        cnt, rt, su);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
-            append_command<TB>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);
+            append_command<TB, true>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);
         }
         resolve_rep_draw(x, p, t, gid, r);
     }
@@ -624,11 +626,10 @@ template <int R> struct InitL {
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k) {
         const size_t lds = (size_t)(JOB_LDS_WORDS + k * NCW) * 4;
-        if (e->p.mode == RAFT_MODE_TEXTBOOK)
-            step_kernel<R, true><<<e->nblocks, STEP_BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
-        else
-            step_kernel<R, false><<<e->nblocks, STEP_BLOCK, lds, e->stream>>>(e->dp, t0, k,
-                                                                                             e->partials);
+        // a flat log (log_window 0) keeps every slot: the kernel without window checks
+        auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? (e->p.log_window ? step_kernel<R, true, true> : step_kernel<R, true, false>)
+                                                     : (e->p.log_window ? step_kernel<R, false, true> : step_kernel<R, false, false>);
+        kern<<<e->nblocks, STEP_BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
     }
 };
 template <int R> struct PackL {

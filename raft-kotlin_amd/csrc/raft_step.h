@@ -69,9 +69,9 @@ constexpr int GX_ISO = 0, GX_CMDS = 1, GX_S0 = 2, GX_WORDS = 3;
 //   ses   int32 [2][G*R]            primary session of group g: nextIndex / matchIndex towards replica r
 //   spill int32 [2][G*R][R]         every other session row: [(g*R + d) * R + s]
 //   gx    int32 [GX_WORDS][G]       isolation word, commands issued, primary-session owner s0 (-1 none)
-//   log   uint2 [waves][NW][64]     (term, cmd) physical slots, one contiguous block per step-kernel
+//   log   uint2 [waves][64][NW]     (term, cmd) physical slots, one contiguous block per step-kernel
 //                                   wave (GPW = 64 / R groups): physical index j of the replica in
-//                                   lane l of wave w at [w][j & wmask][l]; NW = log_window (a ring
+//                                   lane l of wave w at [w][l][j & wmask]; NW = log_window (a ring
 //                                   of the newest NW slots) or log_cap (every slot, no wrap)
 struct DevParams {
     int32_t* st;
@@ -95,22 +95,17 @@ struct DevParams {
 struct Entry { int32_t term; uint32_t cmd; };
 
 // One replica's log in HBM (the reference's ArrayList, Commons.kt:51): its
-// column of its wave's block [NW][64] of DevParams::log.  A wave's slots are
-// one contiguous region (few pages, whatever the slots its lanes touch), and
-// same-slot entries of a group's replicas are adjacent, so the replicas of a
-// group appending the same index in one step write one contiguous run.
+// row of its wave's block [64][NW] of DevParams::log.  A wave's slots are one
+// contiguous region, and a replica's consecutive physical slots are adjacent,
+// so its appends over successive steps fill the same cache lines.
 struct LogView {
-    uint2* wbase;             // its wave's block (wave-uniform in the step kernel: an SGPR pair)
-    uint32_t col;             // its column: the replica's lane in that wave
-    uint32_t wmask;           // slot of physical index j: j & wmask (row stride 64 entries)
+    uint2* lr;                // slot 0 of this replica's row
+    uint32_t ns, wmask;       // NW slots per replica (the row stride); slot of physical index j: j & wmask
     int32_t cap, W;
-    // a 32-bit per-lane offset from a uniform base: global_load/store with saddr
-    __device__ __forceinline__ uint2* at(int32_t j) const {
-        const uint32_t off = (((uint32_t)j & wmask) << 9) | (col << 3);      // bytes: row * 512 + col * 8
-        return (uint2*)((char*)wbase + off);
-    }
+    template <bool RING = true>
+    __device__ __forceinline__ uint2* at(int32_t j) const { return lr + (RING ? ((uint32_t)j & wmask) : (uint32_t)j); }
     // the view of the replica `d` lanes (replica indices) away in the same group
-    __device__ __forceinline__ LogView lane(int d) const { return LogView{wbase, col + d, wmask, cap, W}; }
+    __device__ __forceinline__ LogView lane(int d) const { return LogView{lr + (int64_t)d * ns, ns, wmask, cap, W}; }
     // a reference access of physical index j is below the retained window
     __device__ __forceinline__ uint64_t miss(int32_t j, int32_t phys) const { return __ballot(j < phys - W); }
 };
@@ -158,6 +153,10 @@ struct Counters {
     }
 #ifdef RAFT_EXP_NO_COUNTERS
     __device__ __forceinline__ void add(uint64_t, int) {}
+#elif defined(RAFT_EXP_NO_MISS)
+    __device__ __forceinline__ void add(uint64_t m, int c) {     // timing experiment only
+        if (c != RAFT_C_LOG_WINDOW_MISS) s[c >> 1] += (uint32_t)__popcll(m) << (16 * (c & 1));
+    }
 #else
     __device__ __forceinline__ void add(uint64_t m, int c) { s[c >> 1] += (uint32_t)__popcll(m) << (16 * (c & 1)); }
 #endif
@@ -240,15 +239,20 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
 // miss: the lanes whose write is a reference access below the window (the
 // overwrite branch, or any textbook write, at i < physLen - W); an append at
 // physLen never is.
-template <bool TB = false>
+// CHK: count window misses (the log is a log_window ring; a flat log never misses).
+// RNG: the log is a ring, so slots are masked (a flat log's never wrap).
+template <bool TB, bool CHK, bool RNG>
 __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
-                                        uint64_t& overflow, uint64_t& miss) {
+                                        uint64_t& overflow, uint64_t& miss, bool chk = true) {
     const int32_t last = n.last, phys = n.phys;
     const uint64_t app = lm(i == last);
     const uint64_t ghost = TB ? 0ull : app & lm(phys != last);   // the stale slot log[last] becomes the last entry
     overflow = TB ? act & lm(i >= lv.cap) : act & app & lm(phys >= lv.cap);
     wrote = act & ~overflow;
-    miss = (TB ? wrote : wrote & ~app) & lv.miss(i, phys);
+    miss = 0;
+    if constexpr (CHK) {
+        if (chk) miss = (TB ? wrote : wrote & ~app) & lv.miss(i, phys);
+    }
     // the one slot the new tail cache needs from HBM
     const uint64_t ld = wrote & (ghost | (lm(i != last) & lm(i >= 1) & lm(i != last - 1)));
     const bool ap = ib(app);
@@ -261,14 +265,14 @@ __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Ent
     // also counts its earlier log stores) only when a load was issued
     if (ld) {
         if (ib(ld)) {
-            const uint2 g = *lv.at(ap ? last : i - 1);
+            const uint2 g = *lv.template at<RNG>(ap ? last : i - 1);
             t1 = ap ? (int32_t)g.x : t1;                    // ghost: log[last] is the new last entry
             c1 = ap ? g.y : c1;
             t2 = ap ? t2 : (int32_t)g.x;                    // overwrite: log[i-1] becomes second-to-last
         }
     }
     const bool w = ib(wrote);
-    if (w) *lv.at((ap && !TB) ? phys : i) = make_uint2((uint32_t)e.term, e.cmd);
+    if (w) *lv.template at<RNG>((ap && !TB) ? phys : i) = make_uint2((uint32_t)e.term, e.cmd);
     n.t1 = w ? t1 : n.t1;
     n.c1 = w ? c1 : n.c1;
     n.t2 = w ? t2 : n.t2;
@@ -278,9 +282,11 @@ __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Ent
 }
 
 // ---- vote() (RaftServer.kt:228-251), applied on the lanes of act ----------
-template <bool TB, class CNT>
+// gapw: the lanes whose log.get(lastIndex - 1) is below the log_window
+// (physLen - lastIndex >= W), for the window-miss count (CHK).
+template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, int32_t rt, int32_t rc, int32_t rli,
-                                             int32_t rlt, int32_t W, CNT& cnt, int32_t& resp_term, uint64_t& granted) {
+                                             int32_t rlt, uint64_t gapw, CNT& cnt, int32_t& resp_term, uint64_t& granted) {
     if constexpr (TB) {
         // textbook: a higher term is adopted whatever the answer (Q5 adopts it
         // only on a grant); grant iff votedFor is free or the candidate and the
@@ -296,7 +302,9 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
         const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));
         granted = elig & ~logrej;
         cnt.add(elig & hasl, RAFT_C_VOTE_LOG_READS);
-        cnt.add(elig & hasl & lm(n.last - 1 < n.phys - W), RAFT_C_LOG_WINDOW_MISS);   // log.get(lastIndex - 1)
+        if constexpr (CHK) {
+            if (gapw) cnt.add(elig & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);     // log.get(lastIndex - 1)
+        }
         cnt.add(granted, RAFT_C_VOTES_GRANTED);
         n.voted = ib(granted) ? rc : n.voted;
         n.fl |= ib(granted & lm(rc != id)) ? follower_sent(n.fl) : 0u;
@@ -309,7 +317,9 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
     const uint64_t up = act & higher & ~logrej;                                 // :237-242
     granted = up | (act & lm(rt == n.term) & lm(n.voted == rc));                // :230
     cnt.add(act & higher & hasl, RAFT_C_VOTE_LOG_READS);
-    cnt.add(act & higher & hasl & lm(n.last - 1 < n.phys - W), RAFT_C_LOG_WINDOW_MISS);   // :233 log.get
+    if constexpr (CHK) {
+        if (gapw) cnt.add(act & higher & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);   // :233 log.get
+    }
     cnt.add(granted, RAFT_C_VOTES_GRANTED);
     const bool u = ib(up);
     n.fl |= u ? follower_sent(n.fl) : 0u;                                       // :241
@@ -330,11 +340,14 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
 // this replica's log[prev+1], valid whenever 0 <= prev+1 < lastIndex); the
 // commit follows leaderCommit only after the consistency check, up to the last
 // entry the request vouches for, and never goes down.
-template <bool TB, class CNT>
+//
+// CHK with chk (wave-uniform): count window misses; the caller may pass
+// chk = false when no access of this call can be below the window.
+template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, const LogView& lv, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
                                                    Entry e, int32_t lcommit, int32_t dprev, int32_t dnext, CNT& cnt,
-                                                   int32_t& resp_term, uint64_t& success) {
+                                                   int32_t& resp_term, uint64_t& success, bool chk = true) {
     if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
     const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
@@ -352,20 +365,25 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
     const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
     const uint64_t thrown = check & lm(prev < 0);
     cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
-    uint64_t miss = act & check & ~thrown & lv.miss(prev, n.phys);              // :276 log.get(prevLogIndex)
+    if constexpr (CHK) {
+        if (chk) cnt.add(act & check & ~thrown & lv.miss(prev, n.phys), RAFT_C_LOG_WINDOW_MISS);   // :276 log.get
+    }
     success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
     uint64_t wrote, ovf, wmiss;
     uint64_t same = 0;                                                          // TB: entry already there
     if constexpr (TB) {
         const uint64_t rd = success & has & lm(prev + 1 < n.last);              // TB: reads log[prev + 1]
-        miss |= rd & lv.miss(prev + 1, n.phys);
+        if constexpr (CHK) {
+            if (chk) cnt.add(rd & lv.miss(prev + 1, n.phys), RAFT_C_LOG_WINDOW_MISS);
+        }
         same = rd & lm(dnext == e.term);
     }
-    log_add<TB>(lv, n, prev + 1, e, success & has & ~same, wrote, ovf, wmiss);  // :278 (Q2, Q10)
+    log_add<TB, CHK, CHK>(lv, n, prev + 1, e, success & has & ~same, wrote, ovf, wmiss, chk);   // :278 (Q2, Q10)
     cnt.add(wrote, RAFT_C_ENTRY_WRITES);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
-    cnt.add(miss, RAFT_C_LOG_WINDOW_MISS);
-    cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);
+    if constexpr (CHK) {
+        if (chk) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                        // the write
+    }
     if constexpr (TB) {
         const int32_t lastNew = prev + 1 + (ib(wrote | same) ? 1 : 0);
         const int32_t cc = max(n.commit, min(lcommit, lastNew));
@@ -376,13 +394,13 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
 }
 
 // ---- appendCommand() (RaftServer.kt:100-107), applied on the lanes of act -
-template <bool TB, class CNT>
+template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ void append_command(Rep n, uint64_t act, const LogView& lv, uint32_t cmd, CNT& cnt) {
     uint64_t wrote, ovf, wmiss;
-    log_add<TB>(lv, n, n.last, Entry{n.term, cmd}, act, wrote, ovf, wmiss);
-    cnt.add(act, RAFT_C_COMMANDS);
-    cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
-    cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                                     // TB only: add(lastIndex) writes slot last
+    log_add<TB, CHK && TB, CHK>(lv, n, n.last, Entry{n.term, cmd}, act, wrote, ovf, wmiss);   // the reference
+    cnt.add(act, RAFT_C_COMMANDS);                                              // appends at physLen: no miss;
+    cnt.add(ovf, RAFT_C_LOG_OVERFLOW);                                          // TB writes slot lastIndex
+    if constexpr (CHK && TB) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);
 }
 
 // ---------------------------------------------------------------------------
@@ -456,6 +474,13 @@ struct Ctx {
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
+    // RING (wave-uniform): some replica of the wave may have a ghost gap
+    // physLen - lastIndex >= W - 1 (its log.get(lastIndex - 1) misses the
+    // window at >= W).  A gap only grows by an overwrite in a tick, which can
+    // reach W - 1 only on a lane of the tick's rare branch, so the flag is set
+    // there (and at launch start) and re-checked at the next tick.
+    bool gapseen;
+    uint2* lr;                // this replica's log row: slot 0 (its wave's block, its lane)
 
     __device__ __forceinline__ uint32_t gbits(uint64_t b) const {
         return (uint32_t)(b >> base) & Lanes<R>::ALL;
@@ -470,11 +495,8 @@ struct Ctx {
     // This replica's log.  The wave's block and the ring's geometry are
     // re-derived from the kernarg segment where they are used (kept live
     // across the step loop they would pin SGPRs, see kernargs()).
-    __device__ __forceinline__ LogView log(const DevParams&) const {
-        const KernArgs kp = kernargs();
-        const uint32_t wave = wg0 / (uint32_t)Lanes<R>::GPW;                     // uniform
-        uint2* wb = kp->log + (((uint64_t)wave * (uint32_t)kp->nslots) << 6);
-        return LogView{wb, (uint32_t)(base + r), kp->wmask, kp->cap, kp->W};
+    __device__ __forceinline__ LogView log(const DevParams& p) const {
+        return LogView{lr, (uint32_t)p.nslots, p.wmask, p.cap, p.W};
     }
 };
 
@@ -554,7 +576,9 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
 
 // TB: RAFT_MODE_TEXTBOOK (include/raft_engine.h), compiled as its own kernel
 // so the reference-parity kernel carries none of it.
-template <int R, bool TB>
+// RING: the log is a log_window ring, so every reference access is checked
+// against the window (a flat log keeps every slot: no access can miss).
+template <int R, bool TB, bool RING>
 struct Stepper {
     using L = Lanes<R>;
     static constexpr int MAJ = L::MAJ;
@@ -627,7 +651,6 @@ struct Stepper {
         const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
         const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
         const uint32_t Lc1 = bcastu(n.c1, sl);
-        const int32_t Llo = bcast(n.phys, sl) - kernargs()->W;          // the leader's window floor
         const uint64_t mtk = lm(tk), mme = lm(c.r == s);
         const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
         uint32_t dw;
@@ -653,8 +676,6 @@ struct Stepper {
         const uint64_t has = pge & lm(i <= Llast);
         cnt.add(run & p0 & plt, RAFT_C_PREV_READS_LEADER);
         cnt.add(run & has, RAFT_C_ENTRY_READS_LEADER);
-        cnt.add(run & p0 & plt & lm(prev < Llo), RAFT_C_LOG_WINDOW_MISS);      // :128 log.get(prevLogIndex)
-        cnt.add(run & has & lm(i - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);         // :131 log.get(i - 1)
         // RAFT_C_APPEND_SKIPPED (run & ~ok) is not counted here: run covers
         // whole groups, so it is R * SESSIONS_TICKED - APPEND_SENT, which the
         // counter reduction derives (reduce_counters_kernel)
@@ -675,12 +696,41 @@ struct Stepper {
         const uint64_t ld2 = run & has & lm(i < Llast);
         const uint64_t ld3 = ok & p0 & lm(prev < n.last - 2);
         const uint64_t ld4 = TB ? ok & has & lm(prev + 1 < n.last - 2) : 0ull;
-        if (ld1 | ld2 | ld3 | ld4) {                                      // rare: tail-cache misses
-            if (ib(ld1)) lpt = (int32_t)ls.at(prev)->x;
-            if (ib(ld2)) lent = *ls.at(i - 1);
-            if (ib(ld3)) dpt = (int32_t)lv.at(prev)->x;
-            if (TB && ib(ld4)) dnt = (int32_t)lv.at(prev + 1)->x;
+        // Window misses (RING).  A ring slot is lost only far below physLen:
+        // while no replica of the wave has a ghost gap physLen - lastIndex of
+        // W - 1 or more (c.gapseen clear), each access of the tick that can
+        // miss -- the leader's log[prev] and log[i - 1], this replica's
+        // log[prev] and its write at prev + 1 (TB: its read of log[prev + 1])
+        // -- is more than two slots below its owner's lastIndex, i.e. on a
+        // lane of ld1 / ld2 / ld3 / ld4, or it is the overwrite of slot 0 by
+        // an entry with prev == -1 (m1).  So the exact accounting runs only
+        // with one of those (the rare branch below), or while c.gapseen is set.
+        bool wchk = false;
+        uint64_t m1 = 0;
+        if constexpr (RING) {
+            m1 = run & pge & ~p0 & has;                                   // prev == -1 with an entry: SALU only
+            if (c.gapseen) {                                              // rare: re-check the wave's gaps
+                c.gapseen = lm(n.phys - n.last >= p.W - 1) != 0;
+                wchk = c.gapseen;
+            }
+        }
+        if (ld1 | ld2 | ld3 | ld4 | m1) {                                 // rare: tail-cache misses
+            if (ib(ld1)) lpt = (int32_t)ls.template at<RING>(prev)->x;
+            if (ib(ld2)) lent = *ls.template at<RING>(i - 1);
+            if (ib(ld3)) dpt = (int32_t)lv.template at<RING>(prev)->x;
+            if (TB && ib(ld4)) dnt = (int32_t)lv.template at<RING>(prev + 1)->x;
             asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt), "v"(dnt));   // wait inside the branch
+            if constexpr (RING) wchk = true;
+        }
+        if constexpr (RING) {
+            if (wchk) {                                                   // wave-uniform, rare
+                const int32_t Llo = bcast(n.phys, sl) - p.W;              // the leader's window floor
+                cnt.add(run & p0 & plt & lm(prev < Llo), RAFT_C_LOG_WINDOW_MISS);  // :128 log.get(prevLogIndex)
+                cnt.add(run & has & lm(i - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);     // :131 log.get(i - 1)
+                // an overwrite at prev + 1 leaves a gap physLen - prev - 2: W - 1
+                // or more only if prev < physLen - W
+                if (run & lm(prev < n.phys - p.W)) c.gapseen = true;
+            }
         }
 
         // both directions' losses resolved here: a lane mask of comparisons made
@@ -692,8 +742,8 @@ struct Stepper {
         int32_t rterm;
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
-        append_handler<TB>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
-                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ);
+        append_handler<TB, RING>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ, wchk);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
@@ -764,9 +814,9 @@ struct Stepper {
                 const uint64_t cand = run & lm(!stepdown) & lm(N > C) & lm(N <= Llast);
                 int32_t NT = N - 1 == Llast - 1 ? Lt1 : Lt2;
                 const uint64_t ldn = cand & lm(N - 1 < Llast - 2);
-                cnt.add(cand & lm(N - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);
+                if constexpr (RING) cnt.add(cand & lm(N - 1 < bcast(n.phys, sl) - p.W), RAFT_C_LOG_WINDOW_MISS);
                 if (ldn) {
-                    if (ib(ldn)) NT = (int32_t)ls.at(N - 1)->x;
+                    if (ib(ldn)) NT = (int32_t)ls.template at<RING>(N - 1)->x;
                     asm volatile("" :: "v"(NT));
                 }
                 const uint64_t adv = cand & lm(NT == Lterm);
@@ -802,7 +852,7 @@ struct Stepper {
     template <bool STAGED = false>
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
                                                       uint32_t& vtodo, uint32_t send, int32_t qt, int32_t qli,
-                                                      int32_t qlt) {
+                                                      int32_t qlt, uint64_t gapw) {
         const int r = c.r;
         const bool vr = vtodo != 0;
         const int s = vr ? __builtin_ctz(vtodo) : 0;
@@ -820,7 +870,7 @@ struct Stepper {
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
-        vote_handler<TB>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, kernargs()->W, cnt, rterm, granted);
+        vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, cnt, rterm, granted);
         const uint64_t lresp = act & lost(p, c, s, r, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
@@ -906,7 +956,10 @@ struct Stepper {
             qli = n.last;
             qlt = n.last != 0 ? n.t1 : 0;
             cnt.add((sr | resend) & lm(n.last != 0), RAFT_C_VOTE_LOG_READS);
-            cnt.add((sr | resend) & lm(n.last != 0) & lm(n.last - 1 < n.phys - kernargs()->W), RAFT_C_LOG_WINDOW_MISS);
+            if constexpr (RING) {
+                if (c.gapseen)
+                    cnt.add((sr | resend) & lm(n.last != 0) & lm(n.last - 1 < n.phys - p.W), RAFT_C_LOG_WINDOW_MISS);
+            }
             cnt.add(sr, RAFT_C_ROUNDS);
         }
         start_sessions(p, c, n, sstart, cnt);
@@ -986,23 +1039,29 @@ struct Stepper {
         // runtime s), so the wave runs as many rounds as its busiest group has
         // senders -- usually one -- with one handler per destination lane.
         uint32_t vtodo = c.gbits(__ballot(send != 0));
+        // RING: the replicas whose log.get(lastIndex - 1) is below the window
+        // (the vote handlers do not touch the logs, so once per phase)
+        uint64_t gapw = 0;
+        if constexpr (RING) {
+            if (c.gapseen && __ballot(vtodo != 0)) gapw = lm(n.phys - n.last >= p.W);
+        }
         if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
             // the job lanes do not hold the first sender's chunk (R < 4): one
             // staging pass serves every round, the first included
             if (__ballot(vtodo != 0)) {
                 stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
                 while (__ballot(vtodo != 0));
             }
         } else if (__ballot(vtodo != 0)) {
-            vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+            vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
             if (__ballot(vtodo != 0)) {                                     // groups with 2+ senders
                 if constexpr (L::SENDERS_STAGED) {
                     stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                    do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                    do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
                     while (__ballot(vtodo != 0));
                 } else {
-                    do vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt);
+                    do vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
                     while (__ballot(vtodo != 0));
                 }
             }
@@ -1074,7 +1133,7 @@ struct Stepper {
             const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
                                 lm(lead != 0);
             const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
-            append_command<TB>(n.rep(), tgt, c.log(p), hw2, cnt);
+            append_command<TB, RING>(n.rep(), tgt, c.log(p), hw2, cnt);
             n.cmdc = inc_if(n.cmdc, cm);
         }
 

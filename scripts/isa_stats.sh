@@ -11,7 +11,7 @@ s = open(f'{d}/raft_engine-hip-amdgcn-amd-amdhsa-gfx950.s').read().split('\n')
 cur = None; st = {}
 for i, l in enumerate(s):
     m = re.match(r'^(_Z\S*' + kn + r'ILi(\d)E\S*):', l)
-    if m: cur = m.group(2); st[cur] = collections.Counter(); continue
+    if m: cur = m.group(2) + ("r" if "Lb1EEE" in l or "Lb0ELb1E" in l else ""); st[cur] = collections.Counter(); continue
     if cur and '; -- End function' in l:
         blk = '\n'.join(s[i:i + 30])
         for k in ['codeLenInByte', 'NumVgprs', 'NumSgprs', 'ScratchSize', 'Occupancy']:
