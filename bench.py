@@ -212,8 +212,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-seconds-1t", type=float, default=5.0, help="target seconds of the single-thread CPU leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target seconds of the SoA leg on every core")
+    ap.add_argument("--cpu-seconds-1t", type=float, default=3.0, help="target seconds of each single-thread leg")
     ap.add_argument("--cpu-chunk", type=int, default=20)
     ap.add_argument("--plan-file", default="",
                     help="write the step-kernel launch sequence (leg, steps) and the workload key as JSON, for "
@@ -224,23 +224,33 @@ def parse_args(argv=None):
 
 
 def cpu_baseline(args, kw, log_cap, total_steps):
-    """Oracle (scalar C restatement of the reference) on a bounded sample of
-    the same workload, on this host's cores (rank 0, N=1 only).  The sample
-    is a contiguous range of the same global groups, run for the same number
-    of steps as the GPU (so logs grow exactly as they do there); its size is
-    calibrated so that the timed part takes about --cpu-seconds."""
+    """The CPU path on a bounded sample of the same workload, on this host's
+    cores (rank 0, N=1 only): the SoA backend (oracle/raft_soa.cpp, the same
+    step laid out as structure-of-arrays, std::thread over groups; `value`)
+    and the scalar oracle (oracle/raft_oracle.c, one object per replica,
+    pthreads over groups), each with every usable core and with one.  Both
+    restate the reference's algorithm (the Kotlin itself cannot run here) and
+    are bit-exact with each other and the engine.  A sample is a contiguous
+    range of the same global groups, run for the same number of steps as the
+    GPU (so logs grow exactly as they do there), sized by a short calibration
+    run to take about --cpu-seconds (--cpu-seconds-1t single-threaded)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = args.cpu_threads or available_cpus()
-    # calibration: a short run of a small sample
-    probe = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=args.cpu_groups)))
-    t0 = time.perf_counter()
-    probe.step(args.cpu_chunk, nthreads=threads, counters=False)
-    rate = args.cpu_groups * args.cpu_chunk / max(1e-6, time.perf_counter() - t0)
-    probe.close()
+    impls = {"soa": O.Soa, "oracle": O.Oracle} if kw.get("mode", 0) == abi.MODE_REFERENCE else {"oracle": O.Oracle}
 
-    def timed(G, nthreads):
-        o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
+    def rate_of(cls, nthreads):
+        probe = cls(abi.make_params(log_cap=log_cap, **dict(kw, G=args.cpu_groups)))
+        t0 = time.perf_counter()
+        probe.step(args.cpu_chunk, nthreads=nthreads, counters=False)
+        r = args.cpu_groups * args.cpu_chunk / max(1e-6, time.perf_counter() - t0)
+        probe.close()
+        return r
+
+    def timed(cls, nthreads, seconds):
+        rate = rate_of(cls, nthreads)
+        G = int(min(kw["G"], max(nthreads * 64, rate * seconds / total_steps)))
+        o = cls(abi.make_params(log_cap=log_cap, **dict(kw, G=G)))
         o.step(args.warmup, nthreads=nthreads, counters=False)
         t0 = time.perf_counter()
         done = 0
@@ -250,20 +260,21 @@ def cpu_baseline(args, kw, log_cap, total_steps):
             done += k
         dt = time.perf_counter() - t0
         o.close()
-        return G * done / dt, dt
+        return {"value": G * done / dt, "unit": "group-steps/s", "cores": nthreads,
+                "sample": f"global groups 0..{G - 1}, the same {total_steps} steps as the GPU "
+                          f"({args.warmup} untimed), {dt:.1f} s"}
 
-    G = int(min(kw["G"], max(threads * 64, rate * args.cpu_seconds / total_steps)))
-    value, dt = timed(G, threads)
-    # the single-thread rate on a smaller sample of the same groups
-    G1 = int(min(kw["G"], max(64, rate / threads * args.cpu_seconds_1t / total_steps)))
-    value1, dt1 = timed(G1, 1)
-    return {"value": value, "unit": "group-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/raft_oracle.c (scalar C restatement of RaftServer.kt/Commons.kt), global groups "
-                      f"0..{G - 1} of the same config for the same {total_steps} steps as the GPU "
-                      f"({args.warmup} untimed), {dt:.1f} s, pthreads over groups",
-            "single_thread": {"value": value1, "unit": "group-steps/s", "cores": 1,
-                              "sample": f"global groups 0..{G1 - 1}, same steps, {dt1:.1f} s"},
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+    legs = {}
+    for name, cls in impls.items():
+        legs[name] = timed(cls, threads, args.cpu_seconds if name == "soa" else args.cpu_seconds / 2)
+        legs[name + "_1t"] = timed(cls, 1, args.cpu_seconds_1t)
+    best = legs["soa"] if "soa" in legs else legs["oracle"]
+    return {"value": best["value"], "unit": "group-steps/s", "cores": threads, "kind": "port",
+            "sample": ("oracle/raft_soa.cpp, the SoA CPU backend (bit-exact with the scalar restatement of "
+                       "RaftServer.kt/Commons.kt), std::thread over groups; " if "soa" in legs else
+                       "oracle/raft_oracle.c (scalar C restatement of RaftServer.kt/Commons.kt), pthreads; ")
+                      + best["sample"],
+            "legs": legs, "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
 
 
 def plan_only(args, world, rank):

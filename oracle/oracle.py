@@ -221,3 +221,75 @@ class Oracle:
         rc = lib().oracle_append_command(self.h, group, replica, cmd)
         if rc != 0:
             raise RuntimeError(rc)
+
+
+# ---- the SoA CPU backend (oracle/raft_soa.cpp): CPU BASELINE only ---------
+SOA_LIB = os.path.join(HERE, "lib", "libsoa.so")
+_soa = None
+
+
+def soa_lib():
+    global _soa
+    if _soa is None:
+        if not os.path.exists(SOA_LIB):
+            build()
+        L = C.CDLL(SOA_LIB)
+        P, I32, I64, U32 = C.POINTER, C.c_int32, C.c_int64, C.c_uint32
+        o = C.c_void_p
+        for name, res, args in [
+            ("soa_create", C.c_int, [P(abi.raft_params), P(o)]),
+            ("soa_destroy", None, [o]),
+            ("soa_step", C.c_int, [o, I32, P(I64), I32]),
+            ("soa_read_state", C.c_int, [o, I64, I64, P(I32)]),
+            ("soa_read_log", C.c_int, [o, I64, I64, P(I32), P(U32)]),
+            ("soa_digest", C.c_uint64, [o]),
+        ]:
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _soa = L
+    return _soa
+
+
+class Soa:
+    """The SoA multithreaded CPU backend: same step as Oracle, other layout."""
+
+    def __init__(self, params: "abi.raft_params"):
+        self.p, self.R, self.G, self.cap = params, params.R, params.G, params.log_cap
+        self.W = abi.group_words(self.R)
+        h = C.c_void_p()
+        rc = soa_lib().soa_create(C.byref(params), C.byref(h))
+        if rc != 0:
+            raise ValueError(f"soa_create failed: {rc}")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            soa_lib().soa_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def step(self, n: int, nthreads: int = 1, counters: bool = True):
+        c = abi.counters_array(n) if counters else None
+        rc = soa_lib().soa_step(self.h, n, abi.ptr(c, C.c_int64) if c is not None else None, nthreads)
+        if rc != 0:
+            raise RuntimeError(rc)
+        return c
+
+    def read_state(self, g0=0, n=None):
+        n = self.G - g0 if n is None else n
+        out = np.zeros((n, self.W), dtype=np.int32)
+        if soa_lib().soa_read_state(self.h, g0, n, abi.ptr(out, C.c_int32)) != 0:
+            raise RuntimeError("soa_read_state")
+        return out
+
+    def read_log(self, g0=0, n=None):
+        n = self.G - g0 if n is None else n
+        t = np.zeros((n, self.R, self.cap), dtype=np.int32)
+        c = np.zeros((n, self.R, self.cap), dtype=np.uint32)
+        if soa_lib().soa_read_log(self.h, g0, n, abi.ptr(t, C.c_int32), abi.ptr(c, C.c_uint32)) != 0:
+            raise RuntimeError("soa_read_log")
+        return t, c
+
+    def digest(self) -> int:
+        return int(soa_lib().soa_digest(self.h))
