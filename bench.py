@@ -204,9 +204,8 @@ def parse_args(argv=None):
                     help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
     ap.add_argument("--log-window", type=int, default=-1,
-                    help="ring slots per replica (power of two; 0 = keep every physical slot); default: 256 for "
-                         "configs 2 and 3, whose log accesses stay within 48 slots of physLen, 0 for config 5, "
-                         "whose ghost-tail gaps reach thousands of slots (DESIGN.md §4.2)")
+                    help="ring slots per replica (power of two; 0 = keep every physical slot); default: every slot "
+                         "while that fits 60%% of HBM, else 256 for configs 2 and 3 (DESIGN.md §4.2)")
     ap.add_argument("--reduce-every", type=int, default=512,
                     help="steps per counter all-reduce (rounded to whole launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -339,7 +338,15 @@ def main():
     # physical slots a replica can fill: ~0.3 per step at config 3's command
     # rate, up to one per step where every leader takes a command each step
     log_cap = args.log_cap or int(64 + (1.0 if kw["cmd_ppm"] >= 1_000_000 else 0.3) * total_steps)
-    window = args.log_window if args.log_window >= 0 else {2: 256, 3: 256, 5: 0}[args.config]
+    window = args.log_window
+    if window < 0:
+        # every physical slot (no window checks in the kernel) while that log
+        # fits in 60 % of this GPU's HBM; else the 256-slot ring (configs 2
+        # and 3 never access more than 48 slots below physLen; config 5's
+        # ghost-tail gaps reach thousands of slots, so it is always flat)
+        flat = -(-G_local // (64 // R)) * 64 * log_cap * 8
+        hbm = torch.cuda.get_device_properties(dev).total_memory
+        window = 0 if args.config == 5 or flat <= 0.6 * hbm else 256
     log_cap = max(log_cap, window)                          # the window never exceeds the physLen limit
     L = launch_length(args.steps, args.steps_per_launch)   # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce

@@ -202,7 +202,6 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
     // previous step's log stores, so each step would start by waiting for them.
     __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
-    c.gapseen = RING && __ballot(live && n.phys - n.last >= p.W - 1) != 0;
     __syncthreads();                                                      // counter rows zeroed
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;

@@ -243,16 +243,13 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
 // RNG: the log is a ring, so slots are masked (a flat log's never wrap).
 template <bool TB, bool CHK, bool RNG>
 __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
-                                        uint64_t& overflow, uint64_t& miss, bool chk = true) {
+                                        uint64_t& overflow, uint64_t& miss) {
     const int32_t last = n.last, phys = n.phys;
     const uint64_t app = lm(i == last);
     const uint64_t ghost = TB ? 0ull : app & lm(phys != last);   // the stale slot log[last] becomes the last entry
     overflow = TB ? act & lm(i >= lv.cap) : act & app & lm(phys >= lv.cap);
     wrote = act & ~overflow;
-    miss = 0;
-    if constexpr (CHK) {
-        if (chk) miss = (TB ? wrote : wrote & ~app) & lv.miss(i, phys);
-    }
+    miss = CHK ? (TB ? wrote : wrote & ~app) & lv.miss(i, phys) : 0ull;
     // the one slot the new tail cache needs from HBM
     const uint64_t ld = wrote & (ghost | (lm(i != last) & lm(i >= 1) & lm(i != last - 1)));
     const bool ap = ib(app);
@@ -302,9 +299,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
         const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));
         granted = elig & ~logrej;
         cnt.add(elig & hasl, RAFT_C_VOTE_LOG_READS);
-        if constexpr (CHK) {
-            if (gapw) cnt.add(elig & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);     // log.get(lastIndex - 1)
-        }
+        if constexpr (CHK) cnt.add(elig & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);     // log.get(lastIndex - 1)
         cnt.add(granted, RAFT_C_VOTES_GRANTED);
         n.voted = ib(granted) ? rc : n.voted;
         n.fl |= ib(granted & lm(rc != id)) ? follower_sent(n.fl) : 0u;
@@ -317,9 +312,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
     const uint64_t up = act & higher & ~logrej;                                 // :237-242
     granted = up | (act & lm(rt == n.term) & lm(n.voted == rc));                // :230
     cnt.add(act & higher & hasl, RAFT_C_VOTE_LOG_READS);
-    if constexpr (CHK) {
-        if (gapw) cnt.add(act & higher & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);   // :233 log.get
-    }
+    if constexpr (CHK) cnt.add(act & higher & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);   // :233 log.get
     cnt.add(granted, RAFT_C_VOTES_GRANTED);
     const bool u = ib(up);
     n.fl |= u ? follower_sent(n.fl) : 0u;                                       // :241
@@ -341,13 +334,12 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
 // commit follows leaderCommit only after the consistency check, up to the last
 // entry the request vouches for, and never goes down.
 //
-// CHK with chk (wave-uniform): count window misses; the caller may pass
-// chk = false when no access of this call can be below the window.
+// CHK: the log is a log_window ring: mask slots, count window misses.
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, const LogView& lv, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
                                                    Entry e, int32_t lcommit, int32_t dprev, int32_t dnext, CNT& cnt,
-                                                   int32_t& resp_term, uint64_t& success, bool chk = true) {
+                                                   int32_t& resp_term, uint64_t& success) {
     if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
     const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
@@ -365,25 +357,19 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
     const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
     const uint64_t thrown = check & lm(prev < 0);
     cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
-    if constexpr (CHK) {
-        if (chk) cnt.add(act & check & ~thrown & lv.miss(prev, n.phys), RAFT_C_LOG_WINDOW_MISS);   // :276 log.get
-    }
+    if constexpr (CHK) cnt.add(act & check & ~thrown & lv.miss(prev, n.phys), RAFT_C_LOG_WINDOW_MISS);   // :276
     success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
     uint64_t wrote, ovf, wmiss;
     uint64_t same = 0;                                                          // TB: entry already there
     if constexpr (TB) {
         const uint64_t rd = success & has & lm(prev + 1 < n.last);              // TB: reads log[prev + 1]
-        if constexpr (CHK) {
-            if (chk) cnt.add(rd & lv.miss(prev + 1, n.phys), RAFT_C_LOG_WINDOW_MISS);
-        }
+        if constexpr (CHK) cnt.add(rd & lv.miss(prev + 1, n.phys), RAFT_C_LOG_WINDOW_MISS);
         same = rd & lm(dnext == e.term);
     }
-    log_add<TB, CHK, CHK>(lv, n, prev + 1, e, success & has & ~same, wrote, ovf, wmiss, chk);   // :278 (Q2, Q10)
+    log_add<TB, CHK, CHK>(lv, n, prev + 1, e, success & has & ~same, wrote, ovf, wmiss);   // :278 (Q2, Q10)
     cnt.add(wrote, RAFT_C_ENTRY_WRITES);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
-    if constexpr (CHK) {
-        if (chk) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                        // the write
-    }
+    if constexpr (CHK) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                 // the write
     if constexpr (TB) {
         const int32_t lastNew = prev + 1 + (ib(wrote | same) ? 1 : 0);
         const int32_t cc = max(n.commit, min(lcommit, lastNew));
@@ -474,12 +460,6 @@ struct Ctx {
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
-    // RING (wave-uniform): some replica of the wave may have a ghost gap
-    // physLen - lastIndex >= W - 1 (its log.get(lastIndex - 1) misses the
-    // window at >= W).  A gap only grows by an overwrite in a tick, which can
-    // reach W - 1 only on a lane of the tick's rare branch, so the flag is set
-    // there (and at launch start) and re-checked at the next tick.
-    bool gapseen;
     uint2* lr;                // this replica's log row: slot 0 (its wave's block, its lane)
 
     __device__ __forceinline__ uint32_t gbits(uint64_t b) const {
@@ -696,41 +676,17 @@ struct Stepper {
         const uint64_t ld2 = run & has & lm(i < Llast);
         const uint64_t ld3 = ok & p0 & lm(prev < n.last - 2);
         const uint64_t ld4 = TB ? ok & has & lm(prev + 1 < n.last - 2) : 0ull;
-        // Window misses (RING).  A ring slot is lost only far below physLen:
-        // while no replica of the wave has a ghost gap physLen - lastIndex of
-        // W - 1 or more (c.gapseen clear), each access of the tick that can
-        // miss -- the leader's log[prev] and log[i - 1], this replica's
-        // log[prev] and its write at prev + 1 (TB: its read of log[prev + 1])
-        // -- is more than two slots below its owner's lastIndex, i.e. on a
-        // lane of ld1 / ld2 / ld3 / ld4, or it is the overwrite of slot 0 by
-        // an entry with prev == -1 (m1).  So the exact accounting runs only
-        // with one of those (the rare branch below), or while c.gapseen is set.
-        bool wchk = false;
-        uint64_t m1 = 0;
-        if constexpr (RING) {
-            m1 = run & pge & ~p0 & has;                                   // prev == -1 with an entry: SALU only
-            if (c.gapseen) {                                              // rare: re-check the wave's gaps
-                c.gapseen = lm(n.phys - n.last >= p.W - 1) != 0;
-                wchk = c.gapseen;
-            }
-        }
-        if (ld1 | ld2 | ld3 | ld4 | m1) {                                 // rare: tail-cache misses
+        if (ld1 | ld2 | ld3 | ld4) {                                      // rare: tail-cache misses
             if (ib(ld1)) lpt = (int32_t)ls.template at<RING>(prev)->x;
             if (ib(ld2)) lent = *ls.template at<RING>(i - 1);
             if (ib(ld3)) dpt = (int32_t)lv.template at<RING>(prev)->x;
             if (TB && ib(ld4)) dnt = (int32_t)lv.template at<RING>(prev + 1)->x;
             asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt), "v"(dnt));   // wait inside the branch
-            if constexpr (RING) wchk = true;
         }
-        if constexpr (RING) {
-            if (wchk) {                                                   // wave-uniform, rare
-                const int32_t Llo = bcast(n.phys, sl) - p.W;              // the leader's window floor
-                cnt.add(run & p0 & plt & lm(prev < Llo), RAFT_C_LOG_WINDOW_MISS);  // :128 log.get(prevLogIndex)
-                cnt.add(run & has & lm(i - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);     // :131 log.get(i - 1)
-                // an overwrite at prev + 1 leaves a gap physLen - prev - 2: W - 1
-                // or more only if prev < physLen - W
-                if (run & lm(prev < n.phys - p.W)) c.gapseen = true;
-            }
+        if constexpr (RING) {                                             // window misses (every access counted)
+            const int32_t Llo = bcast(n.phys, sl) - p.W;                  // the leader's window floor
+            cnt.add(run & p0 & plt & lm(prev < Llo), RAFT_C_LOG_WINDOW_MISS);  // :128 log.get(prevLogIndex)
+            cnt.add(run & has & lm(i - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);     // :131 log.get(i - 1)
         }
 
         // both directions' losses resolved here: a lane mask of comparisons made
@@ -743,7 +699,7 @@ struct Stepper {
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
         append_handler<TB, RING>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
-                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ, wchk);
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
@@ -814,7 +770,7 @@ struct Stepper {
                 const uint64_t cand = run & lm(!stepdown) & lm(N > C) & lm(N <= Llast);
                 int32_t NT = N - 1 == Llast - 1 ? Lt1 : Lt2;
                 const uint64_t ldn = cand & lm(N - 1 < Llast - 2);
-                if constexpr (RING) cnt.add(cand & lm(N - 1 < bcast(n.phys, sl) - p.W), RAFT_C_LOG_WINDOW_MISS);
+                if constexpr (RING) cnt.add(cand & mme & lm(N - 1 < bcast(n.phys, sl) - p.W), RAFT_C_LOG_WINDOW_MISS);
                 if (ldn) {
                     if (ib(ldn)) NT = (int32_t)ls.template at<RING>(N - 1)->x;
                     asm volatile("" :: "v"(NT));
@@ -956,10 +912,7 @@ struct Stepper {
             qli = n.last;
             qlt = n.last != 0 ? n.t1 : 0;
             cnt.add((sr | resend) & lm(n.last != 0), RAFT_C_VOTE_LOG_READS);
-            if constexpr (RING) {
-                if (c.gapseen)
-                    cnt.add((sr | resend) & lm(n.last != 0) & lm(n.last - 1 < n.phys - p.W), RAFT_C_LOG_WINDOW_MISS);
-            }
+            if constexpr (RING) cnt.add((sr | resend) & lm(n.last != 0) & lm(n.phys - n.last >= p.W), RAFT_C_LOG_WINDOW_MISS);
             cnt.add(sr, RAFT_C_ROUNDS);
         }
         start_sessions(p, c, n, sstart, cnt);
@@ -1043,7 +996,7 @@ struct Stepper {
         // (the vote handlers do not touch the logs, so once per phase)
         uint64_t gapw = 0;
         if constexpr (RING) {
-            if (c.gapseen && __ballot(vtodo != 0)) gapw = lm(n.phys - n.last >= p.W);
+            if (__ballot(vtodo != 0)) gapw = lm(n.phys - n.last >= p.W);
         }
         if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
             // the job lanes do not hold the first sender's chunk (R < 4): one

@@ -3,7 +3,7 @@
 # scripts/variant_sweep.sh (RAFT_ENGINE_LIB selects one; experiments only):
 #   scripts/build_variants.sh "w6:-DRAFT_STEP_WAVES_PER_EU=6" "w8:-DRAFT_STEP_WAVES_PER_EU=8"
 cd "$(dirname "$0")/.."
-rm -f raft-kotlin_amd/lib/libraft_engine_*.so
+for spec in "$@"; do rm -f raft-kotlin_amd/lib/libraft_engine_${spec%%:*}.so; done
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I include $flags \
