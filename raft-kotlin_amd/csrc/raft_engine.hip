@@ -186,7 +186,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
     c.gg0 = (uint32_t)(p.g0 + c.wg0);
     const int64_t idx = g * R + r;
-    c.lr = p.log + ((int64_t)wid * 64 + lane) * p.nslots;               // its wave's block, its row
+    c.lr = p.log + ((int64_t)wid * 64 + lane) * (RING ? p.nslots : p.cap);   // its wave's block, its row
     c.iso = -1;
     c.part = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};

@@ -475,8 +475,10 @@ struct Ctx {
     // This replica's log.  The wave's block and the ring's geometry are
     // re-derived from the kernarg segment where they are used (kept live
     // across the step loop they would pin SGPRs, see kernargs()).
+    // RING = false: a flat log's row stride is log_cap itself (one SGPR fewer)
+    template <bool RING = true>
     __device__ __forceinline__ LogView log(const DevParams& p) const {
-        return LogView{lr, (uint32_t)p.nslots, p.wmask, p.cap, p.W};
+        return LogView{lr, (uint32_t)(RING ? p.nslots : p.cap), p.wmask, p.cap, p.W};
     }
 };
 
@@ -666,7 +668,7 @@ struct Stepper {
         // tick can change a slot another one reads.  The tail caches answer
         // all but: leader log[prev] below its last two slots, an entry other
         // than the leader's newest, own log[prev] below the last two slots.
-        const LogView lv = c.log(p);
+        const LogView lv = c.template log<RING>(p);
         const LogView ls = lv.lane(s - c.r);                              // the leader's log
         int32_t lpt = cached_term(Llast, Lt1, Lt2, prev);
         int32_t dpt = cached_term(n.last, n.t1, n.t2, prev);
@@ -1086,7 +1088,7 @@ struct Stepper {
             const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
                                 lm(lead != 0);
             const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
-            append_command<TB, RING>(n.rep(), tgt, c.log(p), hw2, cnt);
+            append_command<TB, RING>(n.rep(), tgt, c.template log<RING>(p), hw2, cnt);
             n.cmdc = inc_if(n.cmdc, cm);
         }
 
