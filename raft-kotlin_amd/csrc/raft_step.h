@@ -944,6 +944,12 @@ struct Stepper {
 #ifdef RAFT_EXP_CHEAP_JOB
             c.job = u32x4{c.gid() * 0x9E3779B1u ^ c.t, c.t * 0x85EBCA6Bu ^ sub, purpose ^ c.gid(), c.gid() + c.t};
 #else
+#ifndef RAFT_EXP_CONST_PURPOSE
+            // opaque: otherwise the compiler folds the first Philox round for
+            // every lane's constant purpose and keeps those products in VGPRs
+            // across the step loop (R = 7 spilled them to scratch)
+            asm volatile("" : "+v"(purpose));
+#endif
             c.job = draw(p, c.t, c.gid(), purpose, sub);
 #endif
             // stage the wave's jobs in LDS (one ds_write_b128 per lane); a

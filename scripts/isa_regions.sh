@@ -19,7 +19,7 @@ R=sys.argv[1]
 s=open(sys.argv[2]+'/raft_engine-hip-amdgcn-amd-amdhsa-gfx950.s').read().split('\n')
 cur=False; region='PRE'; c=collections.defaultdict(collections.Counter)
 for l in s:
-    if re.match(r'^_Z\S*step_kernelILi%sE\S*:'%R,l): cur=True; continue
+    if re.match(r'^_Z\S*step_kernelILi%sELb0ELb0E\S*:'%R,l): cur=True; continue
     if cur and '; -- End function' in l: break
     if not cur: continue
     m=re.search(r';MARK_(\w+)',l)
