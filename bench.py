@@ -23,6 +23,7 @@ on a side stream.  Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib
 import json
 import os
@@ -49,6 +50,16 @@ VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
 GROUP_BYTES = 4 * 3
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
+KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h")
+
+
+def kernel_source_id() -> str:
+    """Short hash of the step kernel's sources: a PMC row describes one kernel
+    build, so bench.py attaches it only to a run of the same sources."""
+    h = hashlib.sha1()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, "raft-kotlin_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:12]
 
 
 def shard(total: int, world: int, rank: int, scaling: str) -> tuple[int, int]:
@@ -429,7 +440,8 @@ def main():
     overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
     wmiss = int(c_all[:, abi.C_INDEX["log_window_miss"]].sum())
     pmc_key = {"config": args.config, "mode": args.mode, "groups": G_local, "launch_steps": L,
-               "warmup": args.warmup, "steps": args.steps, "log_window": window}
+               "warmup": args.warmup, "steps": args.steps, "log_window": window,
+               "kernel_src": kernel_source_id()}
     pmc = load_pmc(dict(pmc_key, leg="timed")) if len(set(timed_plan)) == 1 else None
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     roofline_valu = None

@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
 CALIB_G, CALIB_R = int(os.environ.get("TRAFFIC_GROUPS", "1000000")), 5
 REPLICA_BYTES, GROUP_BYTES = 4 * 13 + 8, 12
-ID_FIELDS = ("config", "mode", "groups", "warmup", "steps", "log_window", "leg", "launch_steps", "stream_steps")
+ID_FIELDS = ("config", "mode", "groups", "warmup", "steps", "log_window", "leg", "launch_steps", "stream_steps",
+             "kernel_src")
 
 
 def dispatches(d):

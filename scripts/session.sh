@@ -19,6 +19,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step bench_default 400 python -u bench.py ${BENCH_ARGS:-}
+[ -n "$SKIP_C5" ] || step bench_c5 300 python -u bench.py --config 5 --groups 100000 --no-cpu-baseline
 [ -n "$SKIP_DIST" ] || { TAG=${TAG:-session}/dist STEPS=512 bash scripts/dist_rehearsal.sh > "$OUT/dist.log" 2>&1; rc=$?; echo "dist rc=$rc" | tee -a "$OUT/status.txt"; [ $rc -eq 0 ] || exit $rc; }
 [ -n "$SKIP_PMC" ] || {
   TAG=${TAG:-session}_d20 ARGS="--steps 20 --warmup 5" bash scripts/pmc_bench.sh; rc=$?; echo "pmc_d20 rc=$rc" | tee -a "$OUT/status.txt"; [ $rc -eq 0 ] || exit $rc
