@@ -140,6 +140,13 @@ __device__ __forceinline__ int32_t inc_if(int32_t x, uint64_t m) {
     asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(y), "=s"(carry) : "v"(x), "s"(m));
     return y;
 }
+// x - 1 on the lanes of m: one v_subbrev_co_u32 (x - 0 - borrow) with the mask as borrow-in
+__device__ __forceinline__ int32_t dec_if(int32_t x, uint64_t m) {
+    int32_t y;
+    uint64_t borrow;
+    asm("v_subbrev_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(y), "=s"(borrow) : "v"(x), "s"(m));
+    return y;
+}
 
 // Step counters of a wave.  add(m, c) adds popcount(m) -- the lanes where
 // counter c's event happened -- into the wave-uniform (SGPR) total of counter
@@ -241,17 +248,21 @@ __device__ __forceinline__ int32_t cached_term(int32_t last, int32_t t1, int32_t
 // physLen never is.
 // CHK: count window misses (the log is a log_window ring; a flat log never misses).
 // RNG: the log is a ring, so slots are masked (a flat log's never wrap).
-template <bool TB, bool CHK, bool RNG>
-__device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Entry e, uint64_t act, uint64_t& wrote,
-                                        uint64_t& overflow, uint64_t& miss) {
+// The caller passes app = lm(i == lastIndex) and ige1 = lm(i >= 1): it has
+// made (or can fold) those comparisons already, and a comparison re-used in
+// another basic block would be re-materialised through a VGPR (lm()).
+// AT_END: i == lastIndex on every lane (appendCommand).
+template <bool TB, bool CHK, bool RNG, bool AT_END = false>
+__device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Entry e, uint64_t act, uint64_t app,
+                                        uint64_t ige1, uint64_t& wrote, uint64_t& overflow, uint64_t& miss) {
     const int32_t last = n.last, phys = n.phys;
-    const uint64_t app = lm(i == last);
+    if constexpr (AT_END) app = ~0ull;
     const uint64_t ghost = TB ? 0ull : app & lm(phys != last);   // the stale slot log[last] becomes the last entry
     overflow = TB ? act & lm(i >= lv.cap) : act & app & lm(phys >= lv.cap);
     wrote = act & ~overflow;
     miss = CHK ? (TB ? wrote : wrote & ~app) & lv.miss(i, phys) : 0ull;
     // the one slot the new tail cache needs from HBM
-    const uint64_t ld = wrote & (ghost | (lm(i != last) & lm(i >= 1) & lm(i != last - 1)));
+    const uint64_t ld = wrote & (ghost | (AT_END ? 0ull : ~app & ige1 & lm(i != last - 1)));
     const bool ap = ib(app);
     // the new tail cache without HBM (every value but the loaded slot's)
     int32_t t1 = e.term;
@@ -262,7 +273,7 @@ __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Ent
     // also counts its earlier log stores) only when a load was issued
     if (ld) {
         if (ib(ld)) {
-            const uint2 g = *lv.template at<RNG>(ap ? last : i - 1);
+            const uint2 g = *lv.template at<RNG>(AT_END ? last : (ap ? last : i - 1));
             t1 = ap ? (int32_t)g.x : t1;                    // ghost: log[last] is the new last entry
             c1 = ap ? g.y : c1;
             t2 = ap ? t2 : (int32_t)g.x;                    // overwrite: log[i-1] becomes second-to-last
@@ -274,16 +285,19 @@ __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Ent
     n.c1 = w ? c1 : n.c1;
     n.t2 = w ? t2 : n.t2;
     if constexpr (TB) n.phys = w ? max(phys, i + 1) : phys;
-    else n.phys = ib(wrote & app) ? phys + 1 : phys;
-    n.last = w ? i + 1 : last;
+    else n.phys = inc_if(phys, wrote & app);
+    n.last = AT_END ? inc_if(last, wrote) : (w ? i + 1 : last);
 }
 
 // ---- vote() (RaftServer.kt:228-251), applied on the lanes of act ----------
 // gapw: the lanes whose log.get(lastIndex - 1) is below the log_window
 // (physLen - lastIndex >= W), for the window-miss count (CHK).
+// hasl: the lanes with lastIndex >= 1 (the caller's mask; no handler of a
+// RequestVote phase changes a log).
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, int32_t rt, int32_t rc, int32_t rli,
-                                             int32_t rlt, uint64_t gapw, CNT& cnt, int32_t& resp_term, uint64_t& granted) {
+                                             int32_t rlt, uint64_t gapw, uint64_t hasl, CNT& cnt, int32_t& resp_term,
+                                             uint64_t& granted) {
     if constexpr (TB) {
         // textbook: a higher term is adopted whatever the answer (Q5 adopts it
         // only on a grant); grant iff votedFor is free or the candidate and the
@@ -295,7 +309,6 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
         n.voted = h ? -1 : n.voted;
         n.role = h ? (int32_t)RAFT_FOLLOWER : n.role;
         const uint64_t elig = act & lm(rt == n.term) & (lm(n.voted == -1) | lm(n.voted == rc));
-        const uint64_t hasl = lm(n.last >= 1);
         const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));
         granted = elig & ~logrej;
         cnt.add(elig & hasl, RAFT_C_VOTE_LOG_READS);
@@ -307,7 +320,6 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
         return;
     }
     const uint64_t higher = lm(rt > n.term);                                    // :229-231
-    const uint64_t hasl = lm(n.last >= 1);
     const uint64_t logrej = hasl & (lm(rlt < n.t1) | (lm(rlt == n.t1) & lm(rli < n.last)));   // :232-236 (Q5)
     const uint64_t up = act & higher & ~logrej;                                 // :237-242
     granted = up | (act & lm(rt == n.term) & lm(n.voted == rc));                // :230
@@ -335,11 +347,14 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
 // entry the request vouches for, and never goes down.
 //
 // CHK: the log is a log_window ring: mask slots, count window misses.
+// at_last = lm(prev + 1 == lastIndex), p0 = lm(prev >= 0): the caller's masks
+// (see log_add).
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, const LogView& lv, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
-                                                   Entry e, int32_t lcommit, int32_t dprev, int32_t dnext, CNT& cnt,
-                                                   int32_t& resp_term, uint64_t& success) {
+                                                   Entry e, int32_t lcommit, int32_t dprev, int32_t dnext,
+                                                   uint64_t at_last, uint64_t p0, CNT& cnt, int32_t& resp_term,
+                                                   uint64_t& success) {
     if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
     const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
@@ -355,7 +370,7 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
         n.commit = ib(cu) ? cc : n.commit;
     }
     const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
-    const uint64_t thrown = check & lm(prev < 0);
+    const uint64_t thrown = check & ~p0;
     cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
     if constexpr (CHK) cnt.add(act & check & ~thrown & lv.miss(prev, n.phys), RAFT_C_LOG_WINDOW_MISS);   // :276
     success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
@@ -366,7 +381,7 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
         if constexpr (CHK) cnt.add(rd & lv.miss(prev + 1, n.phys), RAFT_C_LOG_WINDOW_MISS);
         same = rd & lm(dnext == e.term);
     }
-    log_add<TB, CHK, CHK>(lv, n, prev + 1, e, success & has & ~same, wrote, ovf, wmiss);   // :278 (Q2, Q10)
+    log_add<TB, CHK, CHK>(lv, n, prev + 1, e, success & has & ~same, at_last, p0, wrote, ovf, wmiss);   // :278 (Q2, Q10)
     cnt.add(wrote, RAFT_C_ENTRY_WRITES);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
     if constexpr (CHK) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                 // the write
@@ -383,7 +398,7 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ void append_command(Rep n, uint64_t act, const LogView& lv, uint32_t cmd, CNT& cnt) {
     uint64_t wrote, ovf, wmiss;
-    log_add<TB, CHK && TB, CHK>(lv, n, n.last, Entry{n.term, cmd}, act, wrote, ovf, wmiss);   // the reference
+    log_add<TB, CHK && TB, CHK, true>(lv, n, n.last, Entry{n.term, cmd}, act, ~0ull, 0ull, wrote, ovf, wmiss);   // the reference
     cnt.add(act, RAFT_C_COMMANDS);                                              // appends at physLen: no miss;
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);                                          // TB writes slot lastIndex
     if constexpr (CHK && TB) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);
@@ -453,6 +468,7 @@ struct Ctx {
     int r, base;              // replica index, first lane of the group
     bool live;                // lane holds a real replica (whole groups are live or not)
     int iso;                  // isolated replica this step, -1 if none
+    uint64_t iso_me;          // lanes whose replica is the isolated one (lm(r == iso), made once per step)
     uint32_t part;            // replicas on side B of this step's partition
 
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
@@ -484,9 +500,10 @@ struct Ctx {
 
 // The lanes whose message s -> d is lost (S-7): churn isolation, partition
 // sides, or the drop uniform j = 2*dd + b (word dd, half b); self never lost.
+// d is this lane's replica (c.iso_me is its isolation mask).
 template <int R>
 __device__ __forceinline__ uint64_t lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
-    const uint64_t net = lm(s == c.iso) | lm(d == c.iso) |                      // iso = -1: nobody isolated
+    const uint64_t net = lm(s == c.iso) | c.iso_me |                            // iso = -1: nobody isolated
                          lm(((c.part >> s) ^ (c.part >> d)) & 1u);
     return lm(s != d) & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
 }
@@ -624,7 +641,7 @@ struct Stepper {
     // all destinations at once; responses are replayed in destination order.
     // Predicated, called in wave-uniform control flow.
     template <bool STAGED = false>
-    __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, bool tk, int s,
+    __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, uint64_t mtk, int s,
                                                 Counters& cnt) {
         const int sl = c.src(s);
         // the leader's tick-start snapshot and this destination's drop word,
@@ -633,7 +650,7 @@ struct Stepper {
         const int32_t Lterm = bcast(n.term, sl), Lcommit = bcast(n.commit, sl), Llast = bcast(n.last, sl);
         const int32_t Lt1 = bcast(n.t1, sl), Lt2 = bcast(n.t2, sl);
         const uint32_t Lc1 = bcastu(n.c1, sl);
-        const uint64_t mtk = lm(tk), mme = lm(c.r == s);
+        const uint64_t mme = lm(c.r == s);
         const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
         uint32_t dw;
         if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
@@ -654,6 +671,7 @@ struct Stepper {
         // -1 <= prev < lastIndex, and carries an entry iff also i <= lastIndex.
         const int32_t i = n.nx, prev = i - 2;
         const uint64_t pge = lm(prev >= -1), plt = lm(prev < Llast), p0 = lm(prev >= 0);
+        const uint64_t at_last = lm(prev + 1 == n.last);                  // own log[prev] is the tail (log_add: i == lastIndex)
         const uint64_t ok = run & pge & plt;
         const uint64_t has = pge & lm(i <= Llast);
         cnt.add(run & p0 & plt, RAFT_C_PREV_READS_LEADER);
@@ -671,7 +689,7 @@ struct Stepper {
         const LogView lv = c.template log<RING>(p);
         const LogView ls = lv.lane(s - c.r);                              // the leader's log
         int32_t lpt = cached_term(Llast, Lt1, Lt2, prev);
-        int32_t dpt = cached_term(n.last, n.t1, n.t2, prev);
+        int32_t dpt = ib(at_last) ? n.t1 : n.t2;                          // cached_term(n.last, .., prev)
         int32_t dnt = TB ? cached_term(n.last, n.t1, n.t2, prev + 1) : 0;  // TB: own log[prev+1]
         uint2 lent = make_uint2((uint32_t)Lt1, Lc1);
         const uint64_t ld1 = ok & p0 & lm(prev < Llast - 2);
@@ -701,7 +719,7 @@ struct Stepper {
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
         append_handler<TB, RING>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
-                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, cnt, rterm, succ);
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, cnt, rterm, succ);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
@@ -727,9 +745,9 @@ struct Stepper {
         const uint64_t chk = nd & succ & has;                             // :156-162 (Q9)
         const uint64_t hbk = nd & succ & ~has;                            // :163-164
         const uint64_t nak = nd & ~succ;                                  // :166-167
-        const bool bchk = ib(chk);
-        n.nx += bchk ? 1 : (ib(nak) ? -1 : 0);
-        n.mc = bchk ? (TB ? prev + 2 : mc_old + 1) : (ib(hbk) ? prev + 1 : mc_old);   // TB: the entry's index
+        n.nx = dec_if(inc_if(n.nx, chk), nak);                           // chk and nak are disjoint
+        if constexpr (TB) n.mc = ib(chk) ? prev + 2 : (ib(hbk) ? prev + 1 : mc_old);   // TB: the entry's index
+        else n.mc = ib(hbk) ? prev + 1 : inc_if(mc_old, chk);
         cnt.add(chk, RAFT_C_ENTRIES_ACKED);
         // commit rule, after each acknowledged entry in destination order:
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
@@ -807,19 +825,19 @@ struct Stepper {
     // One RequestVote round: every group with a pending sender delivers the
     // requests of its lowest remaining sender s to all destinations at once.
     // Predicated, called in wave-uniform control flow.
+    // mvr: the lanes of groups with a pending sender (the caller's ballot of
+    // vtodo != 0); hasl: lanes with lastIndex >= 1 (constant over the phase).
     template <bool STAGED = false>
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
-                                                      uint32_t& vtodo, uint32_t send, int32_t qt, int32_t qli,
-                                                      int32_t qlt, uint64_t gapw) {
+                                                      uint32_t& vtodo, uint64_t mvr, uint32_t send, int32_t qt,
+                                                      int32_t qli, int32_t qlt, uint64_t gapw, uint64_t hasl) {
         const int r = c.r;
-        const bool vr = vtodo != 0;
-        const int s = vr ? __builtin_ctz(vtodo) : 0;
+        const int s = ib(mvr) ? __builtin_ctz(vtodo) : 0;
         vtodo &= vtodo - 1u;
         const int sl = c.src(s);
         const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
-        const uint64_t mvr = lm(vr);
         uint32_t dw;
         if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
@@ -828,7 +846,7 @@ struct Stepper {
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
-        vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, cnt, rterm, granted);
+        vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, hasl, cnt, rterm, granted);
         const uint64_t lresp = act & lost(p, c, s, r, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
@@ -877,7 +895,8 @@ struct Stepper {
         const uint64_t t_armed = lm(n.fl & FL_ARMED);
         const int32_t t_el = n.elec - p.P;
         const uint64_t t_fire = t_armed & lm(t_el <= 0);                    // Commons.kt:25-27
-        if (!(t_fire | lm(n.fl & FL_ELECTING))) {
+        const uint64_t electing = lm(n.fl & FL_ELECTING);                   // T does not change it before use
+        if (!(t_fire | electing)) {
             n.elec = ib(t_armed) ? t_el : n.elec;
             send = 0u; sstart = 0; qt = qli = qlt = 0;
         } else {
@@ -887,7 +906,7 @@ struct Stepper {
             f &= fire ? ~FL_ARMED : ~0u;
             n.role = fire ? (int32_t)RAFT_CANDIDATE : n.role;               // RaftServer.kt:182
             cnt.add(t_fire, RAFT_C_TIMEOUTS);
-            const uint64_t electing = lm(f & FL_ELECTING), backoff = lm(f & FL_BACKOFF);
+            const uint64_t backoff = lm(f & FL_BACKOFF);
             const uint64_t start_fire = t_fire & ~electing;                 // offer(CANDIDATE) :184 -> :65
             const uint64_t in_round = electing & ~backoff, in_bo = electing & backoff;
             const int32_t ph = n.phase + (ib(in_round) ? p.P : (ib(in_bo) ? -p.P : 0));   // latch clock :214 / delay :221
@@ -926,11 +945,11 @@ struct Stepper {
         // leader to tick (lowest heartbeat session now) and of the first
         // RequestVote sender.  One Philox evaluation of the wave.
         uint32_t hw0, hw1, hw2;
+        uint32_t vtodo = c.gbits(__ballot(send != 0));                     // the group's RequestVote senders
         {
             const uint32_t hb = c.gbits(__ballot((n.fl & FL_HB) != 0));
-            const uint32_t sd = c.gbits(__ballot(send != 0));
             c.s_tick = hb ? __builtin_ctz(hb) : -1;
-            c.s_vote = sd ? __builtin_ctz(sd) : -1;
+            c.s_vote = vtodo ? __builtin_ctz(vtodo) : -1;
         }
         if constexpr (L::JOBS) {
             uint32_t purpose = RAFT_RNG_HARNESS, sub = 0;
@@ -992,6 +1011,7 @@ struct Stepper {
             }
             n.iso = rem > 0 ? (rem << 8) | rep : 0;
             c.iso = rem > 0 ? rep : -1;
+            c.iso_me = lm(r == c.iso);
         }
 
         c.clk.mark(PH_H);
@@ -999,31 +1019,32 @@ struct Stepper {
         // Each group walks its own senders in ascending order (group-uniform,
         // runtime s), so the wave runs as many rounds as its busiest group has
         // senders -- usually one -- with one handler per destination lane.
-        uint32_t vtodo = c.gbits(__ballot(send != 0));
-        // RING: the replicas whose log.get(lastIndex - 1) is below the window
-        // (the vote handlers do not touch the logs, so once per phase)
-        uint64_t gapw = 0;
-        if constexpr (RING) {
-            if (__ballot(vtodo != 0)) gapw = lm(n.phys - n.last >= p.W);
-        }
-        if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
-            // the job lanes do not hold the first sender's chunk (R < 4): one
-            // staging pass serves every round, the first included
-            if (__ballot(vtodo != 0)) {
+        // the lanes of groups with a pending sender: each round's predicate
+        // and the loop condition (one ballot per round)
+        uint64_t mv = lm(vtodo != 0);
+        if (mv) {
+            // RING: the replicas whose log.get(lastIndex - 1) is below the
+            // window; hasl: lastIndex >= 1 (the vote handlers do not touch the
+            // logs, so both hold for the whole phase)
+            const uint64_t gapw = RING ? lm(n.phys - n.last >= p.W) : 0ull;
+            const uint64_t hasl = lm(n.last >= 1);
+            if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
+                // the job lanes do not hold the first sender's chunk (R < 4):
+                // one staging pass serves every round, the first included
                 stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
-                while (__ballot(vtodo != 0));
-            }
-        } else if (__ballot(vtodo != 0)) {
-            vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
-            if (__ballot(vtodo != 0)) {                                     // groups with 2+ senders
-                if constexpr (L::SENDERS_STAGED) {
-                    stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                    do vote_round<true>(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
-                    while (__ballot(vtodo != 0));
-                } else {
-                    do vote_round(p, c, n, cnt, vtodo, send, qt, qli, qlt, gapw);
-                    while (__ballot(vtodo != 0));
+                do {
+                    vote_round<true>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl);
+                    mv = lm(vtodo != 0);
+                } while (mv);
+            } else {
+                vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl);
+                mv = lm(vtodo != 0);
+                if (mv) {                                                   // groups with 2+ senders
+                    if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
+                    do {
+                        vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl);
+                        mv = lm(vtodo != 0);
+                    } while (mv);
                 }
             }
         }
@@ -1059,27 +1080,30 @@ struct Stepper {
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
         uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
         // the first round peeled: the common case runs no loop (a loop makes
-        // the compiler carry the counters in VGPRs and copy the node per round)
-        if (__ballot(todo != 0)) {
+        // the compiler carry the counters in VGPRs and copy the node per round).
+        // mt: the lanes of groups with a session left to tick (each round's
+        // predicate and the loop condition, one ballot per round)
+        uint64_t mt = lm(todo != 0);
+        if (mt) {
             {
                 // R = 2: the job lanes do not hold the first leader's chunk,
                 // so one staging pass serves every round, the first included
                 constexpr bool FIRST_STAGED = L::SENDERS_STAGED && !L::TICK_JOB;
                 if constexpr (FIRST_STAGED) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
-                const bool tk = todo != 0;
-                const int s = tk ? __builtin_ctz(todo) : 0;
+                const int s = ib(mt) ? __builtin_ctz(todo) : 0;
                 todo &= todo - 1u;
-                tick<FIRST_STAGED>(p, c, n, tk, s, cnt);
+                tick<FIRST_STAGED>(p, c, n, mt, s, cnt);
             }
-            if (__ballot(todo != 0)) {                                      // 2+ sessions (rare)
+            mt = lm(todo != 0);
+            if (mt) {                                                       // 2+ sessions (rare)
                 constexpr bool ALL = L::SENDERS_STAGED;
                 if constexpr (ALL && L::TICK_JOB) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
                 do {
-                    const bool tk = todo != 0;
-                    const int s = tk ? __builtin_ctz(todo) : 0;
+                    const int s = ib(mt) ? __builtin_ctz(todo) : 0;
                     todo &= todo - 1u;
-                    tick<ALL>(p, c, n, tk, s, cnt);
-                } while (__ballot(todo != 0));
+                    tick<ALL>(p, c, n, mt, s, cnt);
+                    mt = lm(todo != 0);
+                } while (mt);
             }
         }
 
