@@ -190,6 +190,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.iso = -1;
     c.iso_me = 0;
     c.part = 0;
+    c.part_me = 0;
     c.job = u32x4{0u, 0u, 0u, 0u};
     c.tw = c.dwt = c.dwv = 0u;
     c.jl = lds + wib * 256;
@@ -228,6 +229,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
                 c.part = 0;
             }
         }
+        c.part_me = lm((c.part >> c.r) & 1u);                           // made each step: not loop-carried
         Counters cnt;
         cnt.clear();
         Stepper<R, TB, RING>::step(p, c, n, cnt);

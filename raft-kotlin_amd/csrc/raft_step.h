@@ -470,6 +470,7 @@ struct Ctx {
     int iso;                  // isolated replica this step, -1 if none
     uint64_t iso_me;          // lanes whose replica is the isolated one (lm(r == iso), made once per step)
     uint32_t part;            // replicas on side B of this step's partition
+    uint64_t part_me;         // lanes whose replica is on side B (lm(part >> r & 1), made once per step)
 
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
     uint32_t* jl;             // the wave's LDS staging of the job words, [64 lanes][4]
@@ -478,8 +479,12 @@ struct Ctx {
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
     uint2* lr;                // this replica's log row: slot 0 (its wave's block, its lane)
 
+    // opaque result: tested against 0, (b >> base) & ALL would be rewritten as
+    // b & (ALL << base) != 0 with the mask ANDs moved from SALU to VALU
     __device__ __forceinline__ uint32_t gbits(uint64_t b) const {
-        return (uint32_t)(b >> base) & Lanes<R>::ALL;
+        uint32_t g = (uint32_t)(b >> base) & Lanes<R>::ALL;
+        asm("" : "+v"(g));
+        return g;
     }
     __device__ __forceinline__ int src(int s) const { return base + s; }
     // derived on demand instead of held in VGPRs (register pressure)
@@ -500,11 +505,12 @@ struct Ctx {
 
 // The lanes whose message s -> d is lost (S-7): churn isolation, partition
 // sides, or the drop uniform j = 2*dd + b (word dd, half b); self never lost.
-// d is this lane's replica (c.iso_me is its isolation mask).
+// d is this lane's replica (c.iso_me, c.part_me are its isolation and
+// partition-side masks).
 template <int R>
 __device__ __forceinline__ uint64_t lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
     const uint64_t net = lm(s == c.iso) | c.iso_me |                            // iso = -1: nobody isolated
-                         lm(((c.part >> s) ^ (c.part >> d)) & 1u);
+                         (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
     return lm(s != d) & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
 }
 
@@ -662,6 +668,10 @@ struct Stepper {
             if (ib(swap)) {
                 if (n.s0 >= 0) spill_store(p, c, n, n.s0);
                 spill_load(p, c, n, s);
+                // wait for the loads here: consumed after the branch, they
+                // would put a vmcnt wait (which also counts this tick's log
+                // store) on the common path
+                asm volatile("" :: "v"(n.nx), "v"(n.mc));
             }
         }
         n.s0 = ib(swap) ? s : n.s0;
@@ -732,13 +742,13 @@ struct Stepper {
         const bool stepdown = c.gbits(hib) != 0;
         if (hib) {                                                        // wave-uniform, rare
             const uint32_t dl = c.gbits(delivered);
-            bool sd = false;
 #pragma unroll
             for (int q = 0; q < R; ++q) {
                 const int32_t rq = bcast(rterm, c.src(q));
-                if (((dl >> q) & 1u) && rq > T) { T = rq; if (c.r == q) sd = true; }
+                const uint64_t up = lm((dl >> q) & 1u) & lm(rq > T);
+                T = ib(up) ? rq : T;
+                sdb |= up & L::lanes_of(q);                               // response q stepped down
             }
-            sdb = lm(sd);
         }
         const int32_t mc_old = n.mc;
         const uint64_t nd = delivered & ~sdb;
