@@ -243,7 +243,10 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
 #pragma unroll
         for (int cw = 0; cw < NCW; ++cw) v = (uint32_t)raft_writelane((int32_t)cnt.s[cw], cw, (int32_t)v);
         // < 2^16 per half per workgroup: a wave counts < 2^13 events of a kind per step
-        if (lane < NCW) __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // lanes 0 .. NCW-1 as a constant lane mask (lane < NCW would be a compare
+        // hoisted out of the loop and spilled)
+        if (ib((1ull << NCW) - 1))
+            __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         c.clk.mark(PH_CNT);
     }
     __syncthreads();

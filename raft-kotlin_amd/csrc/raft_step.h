@@ -174,6 +174,15 @@ struct NoCounters {
     __device__ __forceinline__ void add(uint64_t, int) {}
 };
 
+// drop_ppm == 0 (no drop draws at all), tested per use on an opaque copy of
+// the threshold: made once, the compiler keeps it as a lane mask live across
+// the step loop, spilled into a VGPR lane and reloaded in every phase
+__device__ __forceinline__ bool no_drops(const DevParams& p) {
+    uint32_t thr = p.drop_thr16;
+    asm("" : "+s"(thr));
+    return thr == 0;
+}
+
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
     return philox4x32_10(c0, gid, purpose, sub, p.key0, p.key1);
 }
@@ -544,7 +553,7 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int 
 template <int R, bool HAVE_JOB>
 __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, uint64_t act,
                                               int s, uint32_t prefetched, int s_job) {
-    if (p.drop_thr16 == 0) return 0u;
+    if (no_drops(p)) return 0u;
     uint32_t w = 0;
     uint64_t need = act;
     if constexpr (HAVE_JOB) {
@@ -659,7 +668,7 @@ struct Stepper {
         const uint64_t mme = lm(c.r == s);
         const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
         uint32_t dw;
-        if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
+        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
         else dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
         n.fl &= ib(mtk & ~run & mme) ? ~FL_HB : ~0u;                      // :117 cancel() (S-10)
         cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
@@ -826,7 +835,7 @@ struct Stepper {
     // (job_drop_word(c, s, s)) instead of one direct pass each.  Called in
     // wave-uniform control flow.
     __device__ __forceinline__ static void stage_sender_chunks(const DevParams& p, Ctx<R>& c, uint32_t purpose) {
-        if (p.drop_thr16 == 0) return;
+        if (no_drops(p)) return;
         const u32x4 w = draw(p, c.t, c.gid(), purpose, (uint32_t)c.r);
         *(uint4*)&c.jl[(c.base + c.r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
         asm volatile("" ::: "memory");
@@ -849,7 +858,7 @@ struct Stepper {
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
         uint32_t dw;
-        if constexpr (STAGED) dw = p.drop_thr16 == 0 ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
+        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t lreq = mine & lost(p, c, s, r, dw, 0);       // retry{} swallows, Commons.kt:41
@@ -902,8 +911,9 @@ struct Stepper {
         uint64_t sstart;
         // a wave where no timer fires and no replica is electing only counts
         // its armed timers down (most waves in steady state)
+        const int32_t P = p.P;
         const uint64_t t_armed = lm(n.fl & FL_ARMED);
-        const int32_t t_el = n.elec - p.P;
+        const int32_t t_el = n.elec - P;
         const uint64_t t_fire = t_armed & lm(t_el <= 0);                    // Commons.kt:25-27
         const uint64_t electing = lm(n.fl & FL_ELECTING);                   // T does not change it before use
         if (!(t_fire | electing)) {
@@ -919,10 +929,10 @@ struct Stepper {
             const uint64_t backoff = lm(f & FL_BACKOFF);
             const uint64_t start_fire = t_fire & ~electing;                 // offer(CANDIDATE) :184 -> :65
             const uint64_t in_round = electing & ~backoff, in_bo = electing & backoff;
-            const int32_t ph = n.phase + (ib(in_round) ? p.P : (ib(in_bo) ? -p.P : 0));   // latch clock :214 / delay :221
+            const int32_t ph = n.phase + (ib(in_round) ? P : (ib(in_bo) ? -P : 0));   // latch clock :214 / delay :221
             const uint32_t pend = (f >> PEND_SH) & 0xFFu;
             const uint64_t rtick = in_round & lm(pend != 0) & lm(ph < p.round_to);
-            const int32_t rty = n.retry - (ib(rtick) ? p.P : 0);           // retry delay, Commons.kt:43
+            const int32_t rty = n.retry - (ib(rtick) ? P : 0);             // retry delay, Commons.kt:43
             const uint64_t resend = rtick & lm(rty <= 0);
             const uint64_t bo_end = in_bo & lm(ph <= 0);
             const uint64_t restart = bo_end & lm(n.role == RAFT_CANDIDATE); // while (state == CANDIDATE) :191
@@ -1119,12 +1129,13 @@ struct Stepper {
 
         c.clk.mark(PH_A);
         // ---------------- C: client commands (S-11) ----------------
+        // the leaders after A: appendCommand changes no role, so C and K share them
+        const uint64_t isl = lm(n.role == RAFT_LEADER);
+        const uint32_t lead = c.gbits(isl);
         const KernArgs kp = kernargs();
         const uint64_t cmd_thr = kp->cmd_thr32;
         if (cmd_thr) {
             const int32_t cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
-            const uint64_t isl = lm(n.role == RAFT_LEADER);
-            const uint32_t lead = c.gbits(isl);
             const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
                                 lm(lead != 0);
             const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
@@ -1135,8 +1146,6 @@ struct Stepper {
         c.clk.mark(PH_C);
         // ---------------- K: end-of-step observations ----------------
         {
-            const uint64_t isl = lm(n.role == RAFT_LEADER);
-            const uint32_t lead = c.gbits(isl);
             cnt.add(isl, RAFT_C_LEADERS);
             cnt.add(lm(lead != 0) & L::lanes_of(0), RAFT_C_GROUPS_WITH_LEADER);   // one lane per group
             if (lm(__popc(lead) >= 2)) {                                    // rare
@@ -1156,7 +1165,8 @@ struct Stepper {
         if (__ballot((n.fl & FL_DRAW) != 0)) {
             const uint32_t w = timer_word(p, c);
             if (n.fl & FL_DRAW) {
-                n.elec = scale_range(w, p.emin, p.emax);
+                const KernArgs kp = kernargs();
+                n.elec = scale_range(w, kp->emin, kp->emax);
                 n.fl &= ~FL_DRAW;
             }
         }
