@@ -447,17 +447,23 @@ def main():
     roofline_valu = None
     if pmc and pmc.get("valu_per_launch"):
         ips = pmc["valu_per_launch"] / (kern_avg_ms / 1e3) / 1e9
+        clk = pmc.get("effective_clock_ghz") or CLOCK_HZ / 1e9
         roofline_valu = {
             "bound": "valu", "achieved": ips, "peak": VALU_PEAK_GIPS, "unit": "G wave-instructions/s",
             "frac": ips / VALU_PEAK_GIPS,
             "valu_per_wave_step": pmc["valu_per_launch"] / (pmc["waves"] * L),
             "salu_per_wave_step": pmc["salu_per_launch"] / (pmc["waves"] * L),
             "valu_per_simd_cycle": pmc["valu_per_launch"] / (SIMDS * CLOCK_HZ * kern_avg_ms / 1e3),
+            "simd_cycles_per_valu": SIMDS * clk * 1e9 * kern_avg_ms / 1e3 / pmc["valu_per_launch"],
+            "effective_clock_ghz": clk,
             "source": pmc["source"],
-            "note": "SQ_INSTS_VALU of this exact launch (rocprofv3 --pmc, same workload and launch length) / the "
-                    "live average launch time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU "
-                    "instruction (MI355X_MICROARCH.md). The fused kernel is VALU-issue bound: this is its "
-                    "binding roofline",
+            "note": "SQ_INSTS_VALU of this exact launch and kernel build (rocprofv3 --pmc, same workload, launch "
+                    "length and kernel sources) / the live average launch time; peak = 1024 SIMDs x 2.4 GHz / 2 "
+                    "cycles per wave64 VALU instruction (MI355X_MICROARCH.md), the rate of the cheapest (VOP2) "
+                    "instructions. This kernel's mix is mostly VOP3 compares, lane-mask selects and 64-bit "
+                    "multiplies, measured at 4.1-4.7 cycles each on gfx950 (profiles/r1_v7/ubench, DESIGN.md "
+                    "§5.1); simd_cycles_per_valu at about that cost means the VALU pipe is saturated. The fused "
+                    "kernel is VALU-issue bound: this is its binding roofline",
         }
 
     # ---- streaming leg (untimed for `value`): one step per launch, so every

@@ -539,7 +539,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             int32_t rt;
             uint64_t gr;
             vote_handler<TB, true>(x.ref(), __ballot(1), r + 1, q.term, q.candidate_id, q.last_log_index, q.last_log_term,
-                                   __ballot(x.phys - x.last >= p.W), __ballot(x.last >= 1), cnt, rt, gr);
+                                   __ballot(x.phys - x.last >= p.W), __ballot(x.last >= 1), follower_sent(x.fl), cnt,
+                                   rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
@@ -551,7 +552,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, q.term, q.leader_id, pv,
                                                        q.prev_log_term, __ballot(q.has_entry != 0),
                                                        Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
-                                                       __ballot(pv + 1 == x.last), __ballot(pv >= 0), cnt, rt, su);
+                                                       __ballot(pv + 1 == x.last), __ballot(pv >= 0), follower_sent(x.fl),
+                                                       cnt, rt, su);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
             append_command<TB, true>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);

@@ -302,18 +302,19 @@ __device__ __forceinline__ void log_add(const LogView& lv, Rep n, int32_t i, Ent
 // gapw: the lanes whose log.get(lastIndex - 1) is below the log_window
 // (physLen - lastIndex >= W), for the window-miss count (CHK).
 // hasl: the lanes with lastIndex >= 1 (the caller's mask; no handler of a
-// RequestVote phase changes a log).
+// RequestVote phase changes a log).  fsent = follower_sent(fl): made once per
+// phase by the caller (only T and D change FL_ELECTING).
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, int32_t rt, int32_t rc, int32_t rli,
-                                             int32_t rlt, uint64_t gapw, uint64_t hasl, CNT& cnt, int32_t& resp_term,
-                                             uint64_t& granted) {
+                                             int32_t rlt, uint64_t gapw, uint64_t hasl, uint32_t fsent, CNT& cnt,
+                                             int32_t& resp_term, uint64_t& granted) {
     if constexpr (TB) {
         // textbook: a higher term is adopted whatever the answer (Q5 adopts it
         // only on a grant); grant iff votedFor is free or the candidate and the
         // candidate's log is at least as up to date; the self-vote changes nothing
         const uint64_t higher = act & lm(rt > n.term);
         const bool h = ib(higher);
-        n.fl |= ib(higher & lm(n.role != RAFT_FOLLOWER)) ? follower_sent(n.fl) : 0u;
+        n.fl |= ib(higher & lm(n.role != RAFT_FOLLOWER)) ? fsent : 0u;
         n.term = h ? rt : n.term;
         n.voted = h ? -1 : n.voted;
         n.role = h ? (int32_t)RAFT_FOLLOWER : n.role;
@@ -324,7 +325,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
         if constexpr (CHK) cnt.add(elig & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);     // log.get(lastIndex - 1)
         cnt.add(granted, RAFT_C_VOTES_GRANTED);
         n.voted = ib(granted) ? rc : n.voted;
-        n.fl |= ib(granted & lm(rc != id)) ? follower_sent(n.fl) : 0u;
+        n.fl |= ib(granted & lm(rc != id)) ? fsent : 0u;
         resp_term = n.term;
         return;
     }
@@ -336,7 +337,7 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
     if constexpr (CHK) cnt.add(act & higher & hasl & gapw, RAFT_C_LOG_WINDOW_MISS);   // :233 log.get
     cnt.add(granted, RAFT_C_VOTES_GRANTED);
     const bool u = ib(up);
-    n.fl |= u ? follower_sent(n.fl) : 0u;                                       // :241
+    n.fl |= u ? fsent : 0u;                                                     // :241
     n.term = u ? rt : n.term;
     n.voted = u ? rc : n.voted;
     n.role = u ? (int32_t)RAFT_FOLLOWER : n.role;
@@ -357,18 +358,18 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
 //
 // CHK: the log is a log_window ring: mask slots, count window misses.
 // at_last = lm(prev + 1 == lastIndex), p0 = lm(prev >= 0): the caller's masks
-// (see log_add).
+// (see log_add); fsent = follower_sent(fl), made once per phase (see vote_handler).
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, const LogView& lv, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
                                                    Entry e, int32_t lcommit, int32_t dprev, int32_t dnext,
-                                                   uint64_t at_last, uint64_t p0, CNT& cnt, int32_t& resp_term,
-                                                   uint64_t& success) {
+                                                   uint64_t at_last, uint64_t p0, uint32_t fsent, CNT& cnt,
+                                                   int32_t& resp_term, uint64_t& success) {
     if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
     const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
     const bool u = ib(up), f = ib(fol);
-    n.fl |= f ? follower_sent(n.fl) : 0u;
+    n.fl |= f ? fsent : 0u;
     n.term = u ? rt : n.term;
     n.voted = u ? -1 : n.voted;
     n.role = f ? (int32_t)RAFT_FOLLOWER : n.role;
@@ -516,11 +517,13 @@ struct Ctx {
 // sides, or the drop uniform j = 2*dd + b (word dd, half b); self never lost.
 // d is this lane's replica (c.iso_me, c.part_me are its isolation and
 // partition-side masks).
+// mself: the lanes where d == s (the caller's lm(r == s)).
 template <int R>
-__device__ __forceinline__ uint64_t lost(const DevParams& p, const Ctx<R>& c, int s, int d, uint32_t dw, int b) {
+__device__ __forceinline__ uint64_t lost(const DevParams& p, const Ctx<R>& c, int s, uint64_t mself, uint32_t dw,
+                                         int b) {
     const uint64_t net = lm(s == c.iso) | c.iso_me |                            // iso = -1: nobody isolated
                          (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
-    return lm(s != d) & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
+    return ~mself & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
 }
 
 // 16-bit drop uniforms of sender s for this lane as destination d (S-9):
@@ -657,7 +660,7 @@ struct Stepper {
     // Predicated, called in wave-uniform control flow.
     template <bool STAGED = false>
     __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, uint64_t mtk, int s,
-                                                Counters& cnt) {
+                                                uint32_t fs, Counters& cnt) {
         const int sl = c.src(s);
         // the leader's tick-start snapshot and this destination's drop word,
         // all cross-lane reads issued together (one LDS round trip)
@@ -731,14 +734,14 @@ struct Stepper {
         // both directions' losses resolved here: a lane mask of comparisons made
         // in an earlier basic block (before the handler's log store) would be
         // re-materialised through a VGPR
-        const uint64_t lreq = ok & lost(p, c, s, c.r, dw, 0);            // :170-172
+        const uint64_t lreq = ok & lost(p, c, s, mme, dw, 0);            // :170-172
         const uint64_t act = ok & ~lreq;
-        const uint64_t lresp = act & lost(p, c, s, c.r, dw, 1);
+        const uint64_t lresp = act & lost(p, c, s, mme, dw, 1);
         int32_t rterm;
         uint64_t succ;
         // no lane of act throws: ok implies prev >= -1
         append_handler<TB, RING>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
-                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, cnt, rterm, succ);
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, fs, cnt, rterm, succ);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
@@ -825,7 +828,7 @@ struct Stepper {
         n.commit = wb ? C : n.commit;
         n.role = sd ? (int32_t)RAFT_FOLLOWER : n.role;
         if constexpr (TB) n.voted = sd ? -1 : n.voted;                    // TB: a new term has no vote yet
-        n.fl |= (sd && !(n.fl & FL_ELECTING)) ? (FL_ARMED | FL_DRAW) : 0u;
+        n.fl |= sd ? (fs & (FL_ARMED | FL_DRAW)) : 0u;                    // no reset while electing (S-5)
     }
 
     // The drop-word chunk of EVERY sender of the group in one Philox pass of
@@ -849,7 +852,8 @@ struct Stepper {
     template <bool STAGED = false>
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
                                                       uint32_t& vtodo, uint64_t mvr, uint32_t send, int32_t qt,
-                                                      int32_t qli, int32_t qlt, uint64_t gapw, uint64_t hasl) {
+                                                      int32_t qli, int32_t qlt, uint64_t gapw, uint64_t hasl,
+                                                      uint32_t fs) {
         const int r = c.r;
         const int s = ib(mvr) ? __builtin_ctz(vtodo) : 0;
         vtodo &= vtodo - 1u;
@@ -861,19 +865,20 @@ struct Stepper {
         if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
-        const uint64_t lreq = mine & lost(p, c, s, r, dw, 0);       // retry{} swallows, Commons.kt:41
+        const uint64_t mme = lm(r == s);
+        const uint64_t lreq = mine & lost(p, c, s, mme, dw, 0);     // retry{} swallows, Commons.kt:41
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
-        vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, hasl, cnt, rterm, granted);
-        const uint64_t lresp = act & lost(p, c, s, r, dw, 1);
+        vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, hasl, fs, cnt, rterm, granted);
+        const uint64_t lresp = act & lost(p, c, s, mme, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
         // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
         const uint32_t dl = c.gbits(delivered);
         const uint32_t gr = c.gbits(delivered & granted);
         const uint32_t hi = c.gbits(delivered & lm(rterm > st));
-        const bool me = ib(mvr & lm(r == s));
+        const bool me = ib(mvr & mme);
         uint32_t f = n.fl & ~(dl << PEND_SH);
         f += (uint32_t)__popc(dl) << LATCH_SH;                      // :209 countDown()
         f += (uint32_t)__popc(gr) << VOTES_SH;                      // :211
@@ -1048,21 +1053,22 @@ struct Stepper {
             // logs, so both hold for the whole phase)
             const uint64_t gapw = RING ? lm(n.phys - n.last >= p.W) : 0ull;
             const uint64_t hasl = lm(n.last >= 1);
+            const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during V
             if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
                 // the job lanes do not hold the first sender's chunk (R < 4):
                 // one staging pass serves every round, the first included
                 stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
                 do {
-                    vote_round<true>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl);
+                    vote_round<true>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                     mv = lm(vtodo != 0);
                 } while (mv);
             } else {
-                vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl);
+                vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                 mv = lm(vtodo != 0);
                 if (mv) {                                                   // groups with 2+ senders
                     if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
                     do {
-                        vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl);
+                        vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                         mv = lm(vtodo != 0);
                     } while (mv);
                 }
@@ -1105,6 +1111,7 @@ struct Stepper {
         // predicate and the loop condition, one ballot per round)
         uint64_t mt = lm(todo != 0);
         if (mt) {
+            const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during A
             {
                 // R = 2: the job lanes do not hold the first leader's chunk,
                 // so one staging pass serves every round, the first included
@@ -1112,7 +1119,7 @@ struct Stepper {
                 if constexpr (FIRST_STAGED) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
                 const int s = ib(mt) ? __builtin_ctz(todo) : 0;
                 todo &= todo - 1u;
-                tick<FIRST_STAGED>(p, c, n, mt, s, cnt);
+                tick<FIRST_STAGED>(p, c, n, mt, s, fs, cnt);
             }
             mt = lm(todo != 0);
             if (mt) {                                                       // 2+ sessions (rare)
@@ -1121,7 +1128,7 @@ struct Stepper {
                 do {
                     const int s = ib(mt) ? __builtin_ctz(todo) : 0;
                     todo &= todo - 1u;
-                    tick<ALL>(p, c, n, mt, s, cnt);
+                    tick<ALL>(p, c, n, mt, s, fs, cnt);
                     mt = lm(todo != 0);
                 } while (mt);
             }
