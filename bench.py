@@ -157,7 +157,8 @@ def load_pmc(key: dict):
     except (OSError, ValueError):
         return None
     for row in rows:
-        if all(row.get(k) == v for k, v in key.items()):
+        if all(row.get(k) == v for k, v in key.items()) and \
+                row.get("ae_max_entries", 0) == key.get("ae_max_entries", 0):
             return row
     return None
 
@@ -209,6 +210,8 @@ def parse_args(argv=None):
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
                     help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
+    ap.add_argument("--ae-max-entries", type=int, default=0,
+                    help="textbook mode: entries per AppendEntries request (0/1 = one, the reference's shape)")
     ap.add_argument("--steps-per-launch", type=int, default=512,
                     help="upper bound of the lockstep steps fused into one kernel launch (state stays in VGPRs)")
     ap.add_argument("--stream-steps", type=int, default=200,
@@ -363,7 +366,7 @@ def main():
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
     mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
     params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode,
-                             **dict(kw, G=G_local, g0=g0))
+                             ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
@@ -442,6 +445,8 @@ def main():
     pmc_key = {"config": args.config, "mode": args.mode, "groups": G_local, "launch_steps": L,
                "warmup": args.warmup, "steps": args.steps, "log_window": window,
                "kernel_src": kernel_source_id()}
+    if args.ae_max_entries > 1:
+        pmc_key["ae_max_entries"] = args.ae_max_entries
     pmc = load_pmc(dict(pmc_key, leg="timed")) if len(set(timed_plan)) == 1 else None
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     roofline_valu = None
@@ -538,7 +543,8 @@ def main():
                         + {3: ", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step",
                            5: ", 2-way partitions 25 of every 50 steps, 1 command per step to every leader",
                            2: ", no faults, 1/4 command per group-step"}[args.config]
-                        + (", textbook mode" if mode else ""),
+                        + (", textbook mode" if mode else "")
+                        + (f", up to {args.ae_max_entries} entries per AppendEntries" if args.ae_max_entries > 1 else ""),
             "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
             "log_window": window, "hbm_bytes_engine": eng.device_bytes,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
@@ -570,7 +576,8 @@ def main():
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, dict(kw, mode=mode), log_cap, args.warmup + args.steps)
+        out["cpu_baseline"] = cpu_baseline(args, dict(kw, mode=mode, ae_max_entries=args.ae_max_entries), log_cap,
+                                           args.warmup + args.steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -59,6 +59,7 @@ extern "C" {
 
 #define RAFT_MAX_R 8
 #define RAFT_MAX_STEPS_PER_LAUNCH 512   /* steps fused into one kernel launch (LDS counter rows) */
+#define RAFT_MAX_AE_ENTRIES 8           /* textbook mode: entries one AppendEntries request carries */
 
 /* ---- command-injection modes (harness) ---------------- */
 #define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */
@@ -109,7 +110,12 @@ typedef struct raft_params {
                                  * physLen - W is counted in RAFT_C_LOG_WINDOW_MISS; a run with a
                                  * miss is invalid (its results are not the reference's), as with
                                  * RAFT_C_LOG_OVERFLOW.  log_cap stays the physLen limit.          */
-    int32_t  reserved[5];
+    int32_t  ae_max_entries;    /* RAFT_MODE_TEXTBOOK only: the entries one AppendEntries request
+                                 * carries, nextIndex .. up to ae_max_entries of them
+                                 * (greeter.proto:37 `repeated LogEntry entries`).  0 or 1 = one
+                                 * entry, the reference's shape (RaftServer.kt:130-132); at most
+                                 * RAFT_MAX_AE_ENTRIES.  Must be 0 or 1 in reference mode.       */
+    int32_t  reserved[4];
 } raft_params;
 
 /* ---- per-step counters (sum over the engine's groups) ------------------ */

@@ -332,8 +332,12 @@ static void vote_handler(const ctx_t* x, onode_t* n, const raft_vote_req* rq, ra
 }
 
 /* override suspend fun append(request) (RaftServer.kt:253-287).
- * Returns 0, or 1 where the reference throws (Log index < -1). */
-static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq, raft_append_resp* rs) {
+ * Returns 0, or 1 where the reference throws (Log index < -1).
+ * more / nmore: textbook mode with ae_max_entries > 1 only -- the entries the
+ * request carries after its first (log indices prev + 2 ..), applied in order
+ * with the first one's rule while every earlier entry is in place. */
+static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq, raft_append_resp* rs,
+                          const entry_t* more, int32_t nmore) {
     const int tb = x->o->p.mode == RAFT_MODE_TEXTBOOK;
     if (tb && rq->term < n->currentTerm) {         /* textbook: a stale leader is refused, nothing changes */
         rs->term = n->currentTerm; rs->success = 0; rs->status = 0;
@@ -377,6 +381,15 @@ static int append_handler(const ctx_t* x, onode_t* n, const raft_append_req* rq,
         } else {
             int r = olog_add(&n->log, i, e, x->c);
             if (r == 1) { x->c[RAFT_C_ENTRY_WRITES]++; stored = 1; }
+            else if (r == -1) x->c[RAFT_C_LOG_OVERFLOW]++;
+        }
+        for (int32_t k = 0; tb && stored == k + 1 && k < nmore; ++k) {   /* textbook: the further entries */
+            const int32_t j = i + 1 + k;
+            const int hv = j < n->log.lastIndex && olog_get(&n->log, j, &cur);
+            if (hv) olog_touch(&n->log, j, x->c);
+            if (hv && cur.term == more[k].term) { stored++; continue; }
+            int r = olog_add(&n->log, j, more[k], x->c);
+            if (r == 1) { x->c[RAFT_C_ENTRY_WRITES]++; stored++; }
             else if (r == -1) x->c[RAFT_C_LOG_OVERFLOW]++;
         }
     }
@@ -517,6 +530,9 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
         c[RAFT_C_SESSIONS_TICKED]++;
         raft_append_req rq[MAXR];
         int ok[MAXR];
+        entry_t more[MAXR][RAFT_MAX_AE_ENTRIES];   /* textbook: entries after the first */
+        int32_t nent[MAXR];                         /* entries each request carries */
+        const int32_t E = tb && p->ae_max_entries > 1 ? p->ae_max_entries : 1;
         for (int d = 0; d < R; ++d) {              /* build every request first :122-132 */
             int32_t i = L->nextIndex[d];           /* :126 */
             int32_t prev = i - 2;                  /* :127 */
@@ -528,9 +544,17 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
                 else { prevTerm = pe.term; c[RAFT_C_PREV_READS_LEADER]++; olog_touch(&L->log, prev, c); }
             }
             int has = 0;
+            nent[d] = 0;
             if (ok[d] && L->log.lastIndex >= L->nextIndex[d]) {     /* :130 */
                 if (!olog_get(&L->log, i - 1, &ent)) ok[d] = 0;     /* :131 */
-                else { has = 1; c[RAFT_C_ENTRY_READS_LEADER]++; olog_touch(&L->log, i - 1, c); }
+                else { has = 1; nent[d] = 1; c[RAFT_C_ENTRY_READS_LEADER]++; olog_touch(&L->log, i - 1, c); }
+                /* textbook, ae_max_entries > 1: up to E entries, i - 1 .. */
+                for (int32_t k = 1; has && k < E && i - 1 + k < L->log.lastIndex; ++k) {
+                    if (!olog_get(&L->log, i - 1 + k, &more[d][k - 1])) break;
+                    c[RAFT_C_ENTRY_READS_LEADER]++;
+                    olog_touch(&L->log, i - 1 + k, c);
+                    nent[d]++;
+                }
             }
             if (!ok[d]) { c[RAFT_C_APPEND_SKIPPED]++; continue; }
             rq[d].term = L->currentTerm;           /* :137-143 */
@@ -551,7 +575,7 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
             c[RAFT_C_APPEND_SENT]++;
             if (lost(&x, &u, s, d, 0)) { c[RAFT_C_MSG_DROPPED]++; continue; }   /* swallowed :170-172 */
             raft_append_resp rs;
-            if (append_handler(&x, &g->n[d], &rq[d], &rs)) continue;
+            if (append_handler(&x, &g->n[d], &rq[d], &rs, more[d], nent[d] - 1)) continue;
             if (lost(&x, &u, s, d, 1)) { c[RAFT_C_MSG_DROPPED]++; continue; }
             if (tb && rs.term > T) {               /* textbook: adopted after the tick's responses */
                 T = rs.term;
@@ -566,10 +590,10 @@ static void group_step(const struct oracle* o, ogroup_t* g, uint32_t gid, uint32
                 continue;                          /* return@launch: only this coroutine */
             }
             if (rs.success) {                      /* :156-165 (Q9) */
-                if (rq[d].has_entry && tb) {       /* textbook: matchIndex = the acked entry's index */
-                    L->nextIndex[d] += 1;
-                    L->matchIndex[d] = rq[d].prev_log_index + 2;
-                    c[RAFT_C_ENTRIES_ACKED]++;
+                if (rq[d].has_entry && tb) {       /* textbook: matchIndex = the last acked entry's index */
+                    L->nextIndex[d] += nent[d];
+                    L->matchIndex[d] = rq[d].prev_log_index + 1 + nent[d];
+                    c[RAFT_C_ENTRIES_ACKED] += nent[d];
                 } else if (rq[d].has_entry) {
                     L->nextIndex[d] += 1;
                     L->matchIndex[d] += 1;
@@ -656,7 +680,9 @@ int oracle_create(const raft_params* p, oracle_t** out) {
     if (!p || !out || p->R < 1 || p->R > MAXR || p->G < 1 || p->log_cap < 1 || p->heartbeat_ms <= 0 ||
         p->election_min_ms > p->election_max_ms || p->backoff_min_ms > p->backoff_max_ms ||
         (p->mode != RAFT_MODE_REFERENCE && p->mode != RAFT_MODE_TEXTBOOK) || p->log_window < 0 ||
-        (p->log_window && ((p->log_window & (p->log_window - 1)) || p->log_window > p->log_cap)))
+        (p->log_window && ((p->log_window & (p->log_window - 1)) || p->log_window > p->log_cap)) ||
+        p->ae_max_entries < 0 || p->ae_max_entries > RAFT_MAX_AE_ENTRIES ||
+        (p->mode != RAFT_MODE_TEXTBOOK && p->ae_max_entries > 1))
         return RAFT_EINVAL;
     oracle_t* o = (oracle_t*)calloc(1, sizeof(*o));
     if (!o) return RAFT_ENOMEM;
@@ -931,7 +957,7 @@ int oracle_vote(oracle_t* o, int64_t group, int32_t dst, const raft_vote_req* re
 int oracle_append(oracle_t* o, int64_t group, int32_t dst, const raft_append_req* req, raft_append_resp* resp) {
     if (!o || group < 0 || group >= o->G || dst < 0 || dst >= o->R || !req || !resp) return RAFT_EINVAL;
     ctx_t x = { o, o->t, (uint32_t)(o->p.g0 + group), g_scratch_counters, -1, 0 };
-    append_handler(&x, &o->groups[group].n[dst], req, resp);
+    append_handler(&x, &o->groups[group].n[dst], req, resp, NULL, 0);
     return RAFT_OK;
 }
 

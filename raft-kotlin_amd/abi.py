@@ -43,6 +43,7 @@ COUNTER_NAMES = [
 NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
 MAX_STEPS_PER_LAUNCH = 512
+MAX_AE_ENTRIES = 8           # include/raft_engine.h RAFT_MAX_AE_ENTRIES
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
 
 FIELD_NAMES = ["term", "voted", "role", "commit", "last", "phys",
@@ -68,7 +69,7 @@ class raft_params(C.Structure):
         ("partition_period", C.c_int32), ("partition_len", C.c_int32),
         ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
         ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("log_window", C.c_int32),
-        ("reserved", C.c_int32 * 5),
+        ("ae_max_entries", C.c_int32), ("reserved", C.c_int32 * 4),
     ]
 
 

@@ -545,7 +545,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
         } else if (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
             int32_t rt = 0;
-            uint64_t su = 0;
+            uint64_t su = 0, st = 0;
             const int32_t pv = q.prev_log_index;
             const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
             const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
                                                        q.prev_log_term, __ballot(q.has_entry != 0),
                                                        Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
                                                        __ballot(pv + 1 == x.last), __ballot(pv >= 0), follower_sent(x.fl),
-                                                       cnt, rt, su);
+                                                       cnt, rt, su, st);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
             append_command<TB, true>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);
@@ -713,6 +713,9 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_EINVAL, "mode must be RAFT_MODE_REFERENCE or RAFT_MODE_TEXTBOOK");
     if (p->log_window < 0 || (p->log_window & (p->log_window - 1)) || p->log_window > p->log_cap)
         return fail(RAFT_EINVAL, "log_window must be 0 or a power of two <= log_cap");
+    if (p->ae_max_entries < 0 || p->ae_max_entries > RAFT_MAX_AE_ENTRIES ||
+        (p->mode != RAFT_MODE_TEXTBOOK && p->ae_max_entries > 1))
+        return fail(RAFT_EINVAL, "ae_max_entries must be 0..RAFT_MAX_AE_ENTRIES, and 0 or 1 in reference mode");
     if ((p->log_window ? p->log_window : p->log_cap) >= (1 << 23))
         return fail(RAFT_EINVAL, "log slots per replica (log_window, else log_cap) must be < 2^23");
     int ndev = 0;
@@ -745,6 +748,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.churn_thr32 = ppm_thr(p->churn_ppm, 32); d.cmd_thr32 = ppm_thr(p->cmd_ppm, 32);
     d.churn_steps = p->churn_steps; d.part_period = p->partition_period; d.part_len = p->partition_len;
     d.cmd_mode = p->cmd_mode; d.cmd_limit = p->cmd_limit;
+    d.ae_max = p->mode == RAFT_MODE_TEXTBOOK && p->ae_max_entries > 1 ? p->ae_max_entries : 1;
     const int64_t gpb = (int64_t)STEP_WAVES * (64 / p->R);          // groups per step workgroup
     e->nblocks = (int)((G + gpb - 1) / gpb);
     d.GR = G * R;

@@ -90,6 +90,7 @@ struct DevParams {
     uint64_t churn_thr32, cmd_thr32;           // hit32(w) == (w < thr)
     int32_t churn_steps, part_period, part_len;
     int32_t cmd_mode, cmd_limit;
+    int32_t ae_max;                            // entries per AppendEntries request (textbook mode; else 1)
 };
 
 struct Entry { int32_t term; uint32_t cmd; };
@@ -364,7 +365,7 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
                                                    Entry e, int32_t lcommit, int32_t dprev, int32_t dnext,
                                                    uint64_t at_last, uint64_t p0, uint32_t fsent, CNT& cnt,
-                                                   int32_t& resp_term, uint64_t& success) {
+                                                   int32_t& resp_term, uint64_t& success, uint64_t& stored) {
     if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
     const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
@@ -395,6 +396,7 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
     cnt.add(wrote, RAFT_C_ENTRY_WRITES);
     cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
     if constexpr (CHK) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);                 // the write
+    stored = wrote | same;                                                      // TB: the entry is in place
     if constexpr (TB) {
         const int32_t lastNew = prev + 1 + (ib(wrote | same) ? 1 : 0);
         const int32_t cc = max(n.commit, min(lcommit, lastNew));
@@ -725,8 +727,9 @@ struct Stepper {
             if (TB && ib(ld4)) dnt = (int32_t)lv.template at<RING>(prev + 1)->x;
             asm volatile("" :: "v"(lpt), "v"(lent.x), "v"(lent.y), "v"(dpt), "v"(dnt));   // wait inside the branch
         }
+        int32_t Llo = 0;                                                  // RING: the leader's window floor
         if constexpr (RING) {                                             // window misses (every access counted)
-            const int32_t Llo = bcast(n.phys, sl) - p.W;                  // the leader's window floor
+            Llo = bcast(n.phys, sl) - p.W;
             cnt.add(run & p0 & plt & lm(prev < Llo), RAFT_C_LOG_WINDOW_MISS);  // :128 log.get(prevLogIndex)
             cnt.add(run & has & lm(i - 1 < Llo), RAFT_C_LOG_WINDOW_MISS);     // :131 log.get(i - 1)
         }
@@ -738,10 +741,58 @@ struct Stepper {
         const uint64_t act = ok & ~lreq;
         const uint64_t lresp = act & lost(p, c, s, mme, dw, 1);
         int32_t rterm;
-        uint64_t succ;
+        uint64_t succ, stored;
         // no lane of act throws: ok implies prev >= -1
         append_handler<TB, RING>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
-                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, fs, cnt, rterm, succ);
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, fs, cnt, rterm, succ,
+                           stored);
+        // TB, ae_max_entries > 1: the request carries kq = min(E, Llast - i + 1)
+        // entries (greeter.proto:37); the first went through append_handler, the
+        // rest follow with its rule while every earlier one is in place
+        int32_t kq = 1;
+        if constexpr (TB) {
+            const int32_t E = p.ae_max;
+            if (E > 1) {
+                kq = min(E, Llast - i + 1);
+                int32_t nst = ib(stored) ? 1 : 0;                          // entries in place
+                uint64_t in = stored;
+                for (int e = 1; e < E; ++e) {
+                    const uint64_t req = run & has & lm(e < kq);              // entries the leader reads
+                    if (!req) break;                                          // wave-uniform
+                    const int32_t j = prev + 1 + e;
+                    cnt.add(req, RAFT_C_ENTRY_READS_LEADER);
+                    if constexpr (RING) cnt.add(req & lm(j < Llo), RAFT_C_LOG_WINDOW_MISS);
+                    const uint64_t m = in & lm(e < kq);
+                    // the leader's log[j] (its tail cache for its newest entry)
+                    // and this replica's own log[j] term (its tail cache for its
+                    // last two)
+                    uint2 ent = make_uint2((uint32_t)Lt1, Lc1);
+                    int32_t dj = cached_term(n.last, n.t1, n.t2, j);
+                    const uint64_t lde = m & lm(j < Llast - 1);
+                    const uint64_t rd = m & lm(j < n.last);
+                    const uint64_t ldo = rd & lm(j < n.last - 2);
+                    if (lde | ldo) {                                          // rare outside catch-up
+                        if (ib(lde)) ent = *ls.template at<RING>(j);
+                        if (ib(ldo)) dj = (int32_t)lv.template at<RING>(j)->x;
+                        asm volatile("" :: "v"(ent.x), "v"(ent.y), "v"(dj));
+                    }
+                    if constexpr (RING) cnt.add(rd & lv.miss(j, n.phys), RAFT_C_LOG_WINDOW_MISS);
+                    const uint64_t same = rd & lm(dj == (int32_t)ent.x);
+                    uint64_t wrote, ovf, wmiss;
+                    log_add<true, RING, RING>(lv, n.rep(), j, Entry{(int32_t)ent.x, ent.y}, m & ~same,
+                                              lm(j == n.last), lm(j >= 1), wrote, ovf, wmiss);
+                    cnt.add(wrote, RAFT_C_ENTRY_WRITES);
+                    cnt.add(ovf, RAFT_C_LOG_OVERFLOW);
+                    if constexpr (RING) cnt.add(wmiss, RAFT_C_LOG_WINDOW_MISS);
+                    in = same | wrote;
+                    nst = inc_if(nst, in);
+                }
+                // the follower's commit with every entry in place (the handler
+                // applied it for the first; max/min make this idempotent)
+                const int32_t cc = max(n.commit, min(Lcommit, prev + 1 + nst));
+                n.commit = ib(succ & lm(Lcommit > n.commit)) ? cc : n.commit;
+            }
+        }
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
 
@@ -767,10 +818,21 @@ struct Stepper {
         const uint64_t chk = nd & succ & has;                             // :156-162 (Q9)
         const uint64_t hbk = nd & succ & ~has;                            // :163-164
         const uint64_t nak = nd & ~succ;                                  // :166-167
-        n.nx = dec_if(inc_if(n.nx, chk), nak);                           // chk and nak are disjoint
-        if constexpr (TB) n.mc = ib(chk) ? prev + 2 : (ib(hbk) ? prev + 1 : mc_old);   // TB: the entry's index
-        else n.mc = ib(hbk) ? prev + 1 : inc_if(mc_old, chk);
-        cnt.add(chk, RAFT_C_ENTRIES_ACKED);
+        if constexpr (TB) {
+            // TB: nextIndex += the entries acked, matchIndex = the last one's index
+            n.nx = ib(chk) ? n.nx + kq : dec_if(n.nx, nak);
+            n.mc = ib(chk) ? prev + 1 + kq : (ib(hbk) ? prev + 1 : mc_old);
+            cnt.add(chk, RAFT_C_ENTRIES_ACKED);
+            for (int e = 1; e < p.ae_max; ++e) {
+                const uint64_t more = chk & lm(e < kq);
+                if (!more) break;                                         // wave-uniform
+                cnt.add(more, RAFT_C_ENTRIES_ACKED);
+            }
+        } else {
+            n.nx = dec_if(inc_if(n.nx, chk), nak);                       // chk and nak are disjoint
+            n.mc = ib(hbk) ? prev + 1 : inc_if(mc_old, chk);
+            cnt.add(chk, RAFT_C_ENTRIES_ACKED);
+        }
         // commit rule, after each acknowledged entry in destination order:
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;

@@ -22,7 +22,7 @@ OUT_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
 CALIB_G, CALIB_R = int(os.environ.get("TRAFFIC_GROUPS", "1000000")), 5
 REPLICA_BYTES, GROUP_BYTES = 4 * 13 + 8, 12
 ID_FIELDS = ("config", "mode", "groups", "warmup", "steps", "log_window", "leg", "launch_steps", "stream_steps",
-             "kernel_src")
+             "kernel_src", "ae_max_entries")
 
 
 def dispatches(d):

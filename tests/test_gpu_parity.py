@@ -234,6 +234,45 @@ def test_textbook_other_replica_counts(R):
     assert check_log_matching(e, o, f"textbook R={R}") == 0
 
 
+@pytest.mark.parametrize("cfg", [2, 3, "3w", 5])
+def test_textbook_multi_entry_lockstep(cfg):
+    """Textbook mode with up to 8 entries per AppendEntries request
+    (ae_max_entries, greeter.proto:37) against the oracle, bit-exact ("3w": on
+    a 64-slot ring, window misses counted as the oracle counts them)."""
+    win = 64 if cfg == "3w" else 0
+    cfg = 3 if cfg == "3w" else cfg
+    kw = dict(abi.CONFIGS[cfg], mode=abi.MODE_TEXTBOOK, log_window=win, ae_max_entries=8)
+    kw.update({2: dict(G=5_000), 3: dict(G=10_000, churn_ppm=10_000), 5: dict(G=1_000)}[cfg])
+    steps, cap = {2: (400, 200), 3: (1_200, 500), 5: (1_200, 1_400)}[cfg]
+    e, o = pair(log_cap=cap, steps_per_launch=32, **kw)
+    se, ov = run_lockstep(e, o, steps, 100, f"textbook x8 config{cfg}", digest_every=4)
+    assert ov == 0
+    assert check_log_matching(e, o, f"textbook x8 config{cfg}") == 0
+
+
+@pytest.mark.parametrize("E", [2, 3, 5])
+@pytest.mark.parametrize("R", [1, 2, 3, 5, 7, 8])
+def test_textbook_multi_entry_replica_counts(R, E):
+    e, o = pair(R=R, G=2000, seed=300 + R, log_cap=300, drop_ppm=100_000, churn_ppm=20_000, churn_steps=15,
+                cmd_ppm=500_000, partition_period=40, partition_len=10, mode=abi.MODE_TEXTBOOK, ae_max_entries=E)
+    run_lockstep(e, o, 400, 50, f"textbook x{E} R={R}")
+    assert check_log_matching(e, o, f"textbook x{E} R={R}") == 0
+
+
+def test_textbook_multi_entry_kat_on_engine():
+    """tests/test_textbook_cpu.py's hand-derived multi-entry tick, replayed
+    through the engine (write_state + write_log + step)."""
+    import test_textbook_cpu as T
+    o = T._multi_entry_group(4, [(1, 7), (2, 8), (1, 51)])
+    e = RaftEngine(abi.make_params(R=3, G=1, log_cap=64, mode=abi.MODE_TEXTBOOK, ae_max_entries=4))
+    e.write_state(o.read_state())
+    e.write_log(*o.read_log())
+    for _ in range(2):
+        assert np.array_equal(e.step(1), o.step(1)[:, : abi.NUM_COUNTERS])
+        assert np.array_equal(e.read_state(), o.read_state())
+    assert e.digest() == o.digest()
+
+
 FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_size.json")
 
 
