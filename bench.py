@@ -163,6 +163,20 @@ def load_pmc(key: dict):
     return None
 
 
+# resident wave slots of the step kernel on one MI355X: 256 CUs x 4 SIMDs x 6
+# waves (occupancy set by the LDS of a 512-step launch)
+WAVE_SLOTS = 256 * 4 * 6
+
+
+def grid_fill(G: int, R: int) -> str:
+    """How the step kernel's waves (one per 64 // R groups) fill the chip."""
+    waves = -(-G // (64 // R))
+    if waves < WAVE_SLOTS:
+        return (f"{waves} waves < the {WAVE_SLOTS} resident wave slots of one MI355X: the grid cannot fill "
+                f"the chip ({waves / WAVE_SLOTS:.0%} of the slots), so this rate is not the kernel's throughput")
+    return f"{waves} waves = {waves / WAVE_SLOTS:.2f} rounds of the {WAVE_SLOTS} resident wave slots"
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -548,6 +562,8 @@ def main():
             "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
             "log_window": window, "hbm_bytes_engine": eng.device_bytes,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
+            "step_waves_per_rank": -(-G_local // (64 // R)),
+            "grid_fill": grid_fill(G_local, R),
             "counter_allreduce_every": chunk if world > 1 else None,
         },
         "roofline": {
