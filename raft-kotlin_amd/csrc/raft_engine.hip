@@ -7,6 +7,7 @@
 // HBM only for the state load/store at the launch edges, the log slots the
 // handlers read or write, and (rarely) non-primary session rows.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -289,36 +290,77 @@ __global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
     p.st[fidx(p, F_T2, idx)] = (int32_t)b.x;
 }
 
-// counters[k][c] += sum over step workgroups b in this chunk of the 16-bit
-// half (c & 1) of partials[k][c >> 1][b]; grid (chunks, nsteps * NC), the
-// counters zeroed beforehand (int64 atomics: exact and order-independent).
+// counters[k][c] = sum over the step workgroups b of the 16-bit half (c & 1)
+// of partials[k][c >> 1][b], in ONE dispatch with no memset (a memset, an
+// atomic-add reduction and their two dependent dispatch gaps were ~6 % of a
+// 20-step run).  Grid (chunks, nsteps * NCW): each workgroup sums both halves
+// of one packed counter word over a chunk of REDUCE_CHUNK partials (each word
+// is read once) and adds each half, with a ticket of 1 << 48, into that
+// counter's 64-bit accumulator (one returning atomic, no fence: a
+// device-scope fence writes back the L2 and cost more than the whole
+// reduction).  The workgroup that draws a counter's last ticket stores its
+// total outright and resets the accumulator for the next launch.  The first
+// chunk of word 0 zeroes the row's padding.  A step's count is far below 2^48.
 constexpr int REDUCE_CHUNK = 16 * BLOCK;
+constexpr int ACC_TICKET_SH = 48;
+__device__ __forceinline__ uint32_t part_word(const uint32_t* part, int64_t k, int w, int64_t nparts, int b) {
+    return part[(k * NCW + w) * nparts + b];
+}
+__device__ __forceinline__ uint32_t half_of(uint32_t x, int c) { return (x >> (16 * (c & 1))) & 0xFFFFu; }
+// One counter's total: a direct store for a one-chunk grid, else the ticketed accumulator.
+__device__ __forceinline__ void reduce_emit(int64_t* row, int c, unsigned long long s, unsigned long long nch,
+                                            unsigned long long* acc) {
+    if (nch == 1) {
+        row[c] = (int64_t)s;
+        return;
+    }
+    const unsigned long long old = atomicAdd(acc, s + (1ull << ACC_TICKET_SH));
+    if ((old >> ACC_TICKET_SH) != nch - 1) return;
+    row[c] = (int64_t)((old + s) & ((1ull << ACC_TICKET_SH) - 1));
+    atomicExch(acc, 0ull);                                 // ready for the next launch (stream-ordered)
+}
 // APPEND_SKIPPED is derived per workgroup partial as R * SESSIONS_TICKED -
 // APPEND_SENT (the step kernel does not count it, see Stepper::tick).
-__device__ __forceinline__ uint32_t half16(const uint32_t* part, int64_t k, int c, int64_t nparts, int b) {
-    return (part[(k * NCW + (c >> 1)) * nparts + b] >> (16 * (c & 1))) & 0xFFFFu;
-}
 __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* __restrict__ partials, int nparts,
-                                                                int R, int64_t* __restrict__ counters) {
-    __shared__ uint32_t acc[WAVES_PER_BLOCK];
-    const int k = blockIdx.y / NC, c = blockIdx.y % NC;
-    const int b1 = min(nparts, (int)(blockIdx.x + 1) * REDUCE_CHUNK);
-    uint32_t v = 0;                 // < 2^16 * 16 per thread
-    if (c == RAFT_C_APPEND_SKIPPED) {
-        for (int b = blockIdx.x * REDUCE_CHUNK + threadIdx.x; b < b1; b += BLOCK)
-            v += (uint32_t)R * half16(partials, k, RAFT_C_SESSIONS_TICKED, nparts, b) -
-                 half16(partials, k, RAFT_C_APPEND_SENT, nparts, b);
-    } else {
-        for (int b = blockIdx.x * REDUCE_CHUNK + threadIdx.x; b < b1; b += BLOCK) v += half16(partials, k, c, nparts, b);
+                                                                int R, int64_t* __restrict__ counters,
+                                                                unsigned long long* __restrict__ accum) {
+    __shared__ uint32_t acc[2][WAVES_PER_BLOCK];
+    const int k = blockIdx.y / NCW, w = blockIdx.y % NCW;
+    const int c0 = 2 * w, c1 = 2 * w + 1;
+    const int b0 = blockIdx.x * REDUCE_CHUNK;
+    constexpr int SK = RAFT_C_APPEND_SKIPPED;
+    uint32_t lo = 0, hi = 0;        // < 2^19 * 16 per thread
+#pragma unroll
+    for (int i = 0; i < REDUCE_CHUNK / BLOCK; ++i) {      // independent loads
+        const int b = b0 + i * BLOCK + threadIdx.x;
+        if (b < nparts) {
+            const uint32_t x = part_word(partials, k, w, nparts, b);
+            uint32_t d = 0;
+            if (w == SK >> 1)
+                d = (uint32_t)R * half_of(part_word(partials, k, RAFT_C_SESSIONS_TICKED >> 1, nparts, b),
+                                          RAFT_C_SESSIONS_TICKED) -
+                    half_of(part_word(partials, k, RAFT_C_APPEND_SENT >> 1, nparts, b), RAFT_C_APPEND_SENT);
+            lo += c0 == SK ? d : x & 0xFFFFu;
+            hi += c1 == SK ? d : x >> 16;
+        }
     }
-    const uint32_t ws = __ockl_wfred_add_u32(v);   // < 2^16 * REDUCE_CHUNK = 2^28
-    if ((threadIdx.x & 63) == 0) acc[threadIdx.x >> 6] = ws;
+    const uint32_t wl = __ockl_wfred_add_u32(lo), wh = __ockl_wfred_add_u32(hi);   // < 2^19 * 1024 = 2^29
+    if ((threadIdx.x & 63) == 0) {
+        acc[0][threadIdx.x >> 6] = wl;
+        acc[1][threadIdx.x >> 6] = wh;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t s = 0;
-        for (int w = 0; w < WAVES_PER_BLOCK; ++w) s += acc[w];
-        if (s) atomicAdd((unsigned long long*)&counters[(int64_t)k * RAFT_COUNTER_STRIDE + c], (unsigned long long)s);
+    int64_t* row = counters + (int64_t)k * RAFT_COUNTER_STRIDE;
+    if (w == 0 && blockIdx.x == 0 && threadIdx.x >= NC && threadIdx.x < RAFT_COUNTER_STRIDE) row[threadIdx.x] = 0;
+    if (threadIdx.x != 0) return;
+    unsigned long long sl = 0, sh = 0;
+    for (int q = 0; q < WAVES_PER_BLOCK; ++q) {
+        sl += acc[0][q];
+        sh += acc[1][q];
     }
+    const unsigned long long nch = gridDim.x;
+    reduce_emit(row, c0, sl, nch, &accum[(int64_t)k * NC + c0]);
+    if (c1 < NC) reduce_emit(row, c1, sh, nch, &accum[(int64_t)k * NC + c1]);
 }
 
 // canonical export [n][W] of groups [g0, g0+n): one thread per group
@@ -601,6 +643,8 @@ struct raft_engine {
     int nblocks;                // step-kernel workgroups: ceil(G / (STEP_WAVES * (64 / R)))
     uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials
     int64_t* counters_dev;      // [K][STRIDE] scratch
+    int nchunks;                // counter-reduction chunks of REDUCE_CHUNK partials
+    unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
     // step-kernel event timing
     bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
     bool timing;
@@ -631,12 +675,15 @@ template <int R> struct InitL {
     }
 };
 template <int R> struct StepL {
-    static void run(raft_engine* e, uint32_t t0, int k) {
+    static void run(raft_engine* e, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1) {
         const size_t lds = (size_t)(JOB_LDS_WORDS + k * NCW) * 4;
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
         auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? (e->p.log_window ? step_kernel<R, true, true> : step_kernel<R, true, false>)
                                                      : (e->p.log_window ? step_kernel<R, false, true> : step_kernel<R, false, false>);
-        kern<<<e->nblocks, STEP_BLOCK, lds, e->stream>>>(e->dp, t0, k, e->partials);
+        // the launch's own start / stop timestamps (ev0, ev1 nullable): no
+        // marker packets around the dispatch
+        hipExtLaunchKernelGGL(kern, dim3(e->nblocks), dim3(STEP_BLOCK), (uint32_t)lds, e->stream, ev0, ev1, 0u,
+                              e->dp, t0, k, e->partials);
     }
 };
 template <int R> struct PackL {
@@ -763,7 +810,9 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     // sized for the largest launch, so steps_per_launch can change later
     const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;
     const size_t cnt_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * RAFT_COUNTER_STRIDE * 8;
-    e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(log_b);
+    e->nchunks = (e->nblocks + REDUCE_CHUNK - 1) / REDUCE_CHUNK;
+    const size_t acc_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NC * 8;
+    e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (err != hipSuccess) { delete e; return fail(RAFT_EDEVICE, "hipStreamCreate failed"); }
     err = hipMalloc(&e->base, e->bytes);
@@ -779,10 +828,12 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.gx = (int32_t*)b; b += al(gx_b);
     e->partials = (uint32_t*)b; b += al(part_b);
     e->counters_dev = (int64_t*)b; b += al(cnt_b);
+    e->accum = (unsigned long long*)b; b += al(acc_b);
     d.log = (uint2*)b;
     *out = e;
     dispatch_R<InitL>(p->R, e);
-    err = hipStreamSynchronize(e->stream);
+    err = hipMemsetAsync(e->accum, 0, acc_b, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     if (err != hipSuccess) {
         (void)hipFree(e->base);
         (void)hipStreamDestroy(e->stream);
@@ -819,6 +870,18 @@ int raft_engine_destroy(raft_engine* e) {
     return RAFT_OK;
 }
 
+// Grow the timing-event pool to hold `pairs` more launches.  Called when
+// timing is switched on, so a timed region never creates events (64
+// hipEventCreate calls cost ~0.1 ms of host time, 7 % of a 20-step run).
+static int reserve_events(raft_engine* e, size_t pairs) {
+    while (e->ev_used + 2 * pairs > e->ev.size()) {
+        hipEvent_t x;
+        HIP_TRY(hipEventCreate(&x));
+        e->ev.push_back(x);
+    }
+    return RAFT_OK;
+}
+
 int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_dev) {
     if (!e || n_steps < 0) return fail(RAFT_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(e->device));
@@ -828,25 +891,18 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
     }
     for (int32_t done = 0; done < n_steps;) {
         const int k = std::min<int32_t>(e->K, n_steps - done);
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;
         if (e->timing) {
-            if (e->ev_used + 2 > e->ev.size()) {
-                for (int q = 0; q < 64; ++q) {
-                    hipEvent_t x;
-                    HIP_TRY(hipEventCreate(&x));
-                    e->ev.push_back(x);
-                }
-            }
-            HIP_TRY(hipEventRecord(e->ev[e->ev_used], e->stream));
-        }
-        dispatch_R<StepL>(e->p.R, e, (uint32_t)(e->t + done), k);
-        if (e->timing) {
-            HIP_TRY(hipEventRecord(e->ev[e->ev_used + 1], e->stream));
+            if (e->ev_used + 2 > e->ev.size())
+                if (int rc = reserve_events(e, 64)) return rc;
+            ev0 = e->ev[e->ev_used];
+            ev1 = e->ev[e->ev_used + 1];
             e->ev_used += 2;
         }
+        dispatch_R<StepL>(e->p.R, e, (uint32_t)(e->t + done), k, ev0, ev1);
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
-        HIP_TRY(hipMemsetAsync(dst, 0, (size_t)k * RAFT_COUNTER_STRIDE * 8, e->stream));
-        const dim3 rg((unsigned)((e->nblocks + REDUCE_CHUNK - 1) / REDUCE_CHUNK), (unsigned)(k * NC));
-        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, e->p.R, dst);
+        const dim3 rg((unsigned)e->nchunks, (unsigned)(k * NCW));
+        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, e->p.R, dst, e->accum);
         done += k;
     }
     HIP_TRY(hipGetLastError());
@@ -881,6 +937,10 @@ void* raft_engine_stream(raft_engine* e) { return e ? (void*)e->stream : nullptr
 int raft_engine_set_kernel_timing(raft_engine* e, int enable) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     e->timing = enable != 0;
+    if (e->timing) {
+        HIP_TRY(hipSetDevice(e->device));
+        return reserve_events(e, 256);
+    }
     return RAFT_OK;
 }
 

@@ -837,22 +837,47 @@ struct Stepper {
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;
         if (!TB && chk) {                                                 // wave-uniform
-            // bit q of the group's acks, pre-shifted so that one v_bcnt adds
-            // it (as 16 << q) to the popcount: pc >= (16 << q) + MAJ tests
-            // "response q acked and count >= majority" in one compare
-            const uint32_t ck16 = c.gbits(chk) << 4;
-            uint64_t commits = 0;                                         // one lane per increment
-#pragma unroll
-            for (int q = 0; q < R; ++q) {
-                if (!(chk & L::lanes_of(q))) continue;                    // wave-uniform
-                const int32_t cur = ib(L::lanes_upto(q)) ? n.mc : mc_old; // rows after / before response q
-                const uint32_t gt = c.gbits(lm(cur > C));                 // :161
-                const uint32_t pc = __popc(gt) + (ck16 & (16u << q));
-                const uint64_t inc = lm(pc >= (16u << q) + MAJ);          // :162 (whole groups)
+            const uint32_t ck = c.gbits(chk);                             // the group's acked responses
+            // Closed form (common case).  While no row went down (monotone:
+            // an ack raises matchIndex, a nak keeps it), the count of rows
+            // above a fixed C after response q never falls as q grows, so
+            // "some acked q reaches a majority at C = Lcommit" is the test at
+            // the group's LAST acked response q*: rows up to q* as they are
+            // after the tick, the rest as before it.  If fewer than a majority
+            // of rows ends above Lcommit + 1, a second increment is impossible.
+            // Otherwise (a row went down, or a majority ends above Lcommit + 1:
+            // a lagging commitIndex, Q9) the replay below runs.
+            const uint64_t hi2 = run & lm(n.mc > C + 1);                 // (the ticking groups' rows)
+            uint64_t slow = run & lm(n.mc < mc_old);
+            if (hi2) slow |= lm(__popc(c.gbits(hi2)) >= MAJ);             // wave-uniform, rare
+#ifdef RAFT_EXP_COMMIT_REPLAY
+            slow = ~0ull;                                                 // A/B experiment only: always replay
+#endif
+            if (!slow) {
+                const uint64_t upto = lm((ck >> c.r) != 0u);              // rows at or before q*
+                const int32_t cur = ib(upto) ? n.mc : mc_old;
+                const uint64_t inc = lm(__popc(c.gbits(lm(cur > C))) >= MAJ) & lm(ck != 0u);   // :161-162
                 C = inc_if(C, inc);
-                commits |= inc & L::lanes_of(q);                          // disjoint lanes per q
+                cnt.add(inc & L::lanes_of(0), RAFT_C_COMMITS);            // one lane per group
+            } else {
+                // the replay in destination order.  Bit q of the group's acks,
+                // pre-shifted so that one v_bcnt adds it (as 16 << q) to the
+                // popcount: pc >= (16 << q) + MAJ tests "response q acked and
+                // count >= majority" in one compare
+                const uint32_t ck16 = ck << 4;
+                uint64_t commits = 0;                                     // one lane per increment
+#pragma unroll
+                for (int q = 0; q < R; ++q) {
+                    if (!(chk & L::lanes_of(q))) continue;                // wave-uniform
+                    const int32_t cur = ib(L::lanes_upto(q)) ? n.mc : mc_old;   // rows after / before response q
+                    const uint32_t gt = c.gbits(lm(cur > C));             // :161
+                    const uint32_t pc = __popc(gt) + (ck16 & (16u << q));
+                    const uint64_t inc = lm(pc >= (16u << q) + MAJ);      // :162 (whole groups)
+                    C = inc_if(C, inc);
+                    commits |= inc & L::lanes_of(q);                      // disjoint lanes per q
+                }
+                cnt.add(commits, RAFT_C_COMMITS);
             }
-            cnt.add(commits, RAFT_C_COMMITS);
         }
         if constexpr (TB) {
             // textbook commit rule: N = the majority-th largest matchIndex of the
