@@ -132,6 +132,15 @@ __device__ __forceinline__ KernArgs kernargs() {
 // it again: two VALU per ballot.)  Negations are only ever taken inside a
 // positive mask, so dead lanes (inert nodes) never satisfy a predicate.
 __device__ __forceinline__ uint64_t lm(bool cmp) { return __ballot(cmp); }
+// Branch hints for the wave-uniform rare paths: the common path falls through
+// (a taken s_cbranch restarts the wave's instruction fetch).
+#ifdef RAFT_EXP_NO_EXPECT
+#define RARE(x) (x)
+#define LIKELY(x) (x)
+#else
+#define RARE(x) __builtin_expect(!!(x), 0)
+#define LIKELY(x) __builtin_expect(!!(x), 1)
+#endif
 __device__ __forceinline__ bool ib(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 // x + 1 on the lanes of m: one v_addc_co_u32 with the mask as carry-in (the
 // compiler would emit a v_cndmask and a v_add)
@@ -520,11 +529,16 @@ struct Ctx {
 // d is this lane's replica (c.iso_me, c.part_me are its isolation and
 // partition-side masks).
 // mself: the lanes where d == s (the caller's lm(r == s)).
+// lost_net: the network part (isolation, partition) of sender s's messages,
+// made once per round for both directions.  (Skipping its compares in waves
+// with no isolation or partition measured slower: the branches cost more
+// SALU issue than the VALU they save.)
 template <int R>
-__device__ __forceinline__ uint64_t lost(const DevParams& p, const Ctx<R>& c, int s, uint64_t mself, uint32_t dw,
-                                         int b) {
-    const uint64_t net = lm(s == c.iso) | c.iso_me |                            // iso = -1: nobody isolated
-                         (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
+__device__ __forceinline__ uint64_t lost_net(const Ctx<R>& c, int s) {
+    return lm(s == c.iso) | c.iso_me |                                          // iso = -1: nobody isolated
+           (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
+}
+__device__ __forceinline__ uint64_t lost(const DevParams& p, uint64_t net, uint64_t mself, uint32_t dw, int b) {
     return ~mself & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
 }
 
@@ -565,7 +579,7 @@ __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& 
         w = prefetched;
         need = act & lm(s != s_job);
     }
-    if (need) {
+    if (RARE(need)) {
         if (ib(need)) w = drop_word_direct(p, c, purpose, s);
     }
     return w;
@@ -645,7 +659,7 @@ struct Stepper {
             const int32_t cs = bcast(TB ? n.last : n.commit, c.src(s));  // TB: nextIndex = lastIndex + 1
             const uint64_t mst = lm((sb >> s) & 1u);
             const uint64_t msp = mst & lm(n.s0 >= 0) & lm(n.s0 != s);
-            if (msp) {
+            if (RARE(msp)) {
                 if (ib(msp)) spill_store(p, c, n, n.s0);
             }
             const bool st = ib(mst);
@@ -678,7 +692,7 @@ struct Stepper {
         n.fl &= ib(mtk & ~run & mme) ? ~FL_HB : ~0u;                      // :117 cancel() (S-10)
         cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
         const uint64_t swap = run & lm(n.s0 != s);                        // swap the session in (rare)
-        if (swap) {
+        if (RARE(swap)) {
             if (ib(swap)) {
                 if (n.s0 >= 0) spill_store(p, c, n, n.s0);
                 spill_load(p, c, n, s);
@@ -737,9 +751,10 @@ struct Stepper {
         // both directions' losses resolved here: a lane mask of comparisons made
         // in an earlier basic block (before the handler's log store) would be
         // re-materialised through a VGPR
-        const uint64_t lreq = ok & lost(p, c, s, mme, dw, 0);            // :170-172
+        const uint64_t net = lost_net(c, s);
+        const uint64_t lreq = ok & lost(p, net, mme, dw, 0);              // :170-172
         const uint64_t act = ok & ~lreq;
-        const uint64_t lresp = act & lost(p, c, s, mme, dw, 1);
+        const uint64_t lresp = act & lost(p, net, mme, dw, 1);
         int32_t rterm;
         uint64_t succ, stored;
         // no lane of act throws: ok implies prev >= -1
@@ -802,8 +817,9 @@ struct Stepper {
         int32_t T = Lterm;
         uint64_t sdb = 0;                                                 // responses that stepped down
         const uint64_t hib = delivered & lm(rterm > Lterm);
-        const bool stepdown = c.gbits(hib) != 0;
-        if (hib) {                                                        // wave-uniform, rare
+        bool stepdown = false;
+        if (RARE(hib)) {                                                  // wave-uniform, rare
+            stepdown = c.gbits(hib) != 0;
             const uint32_t dl = c.gbits(delivered);
 #pragma unroll
             for (int q = 0; q < R; ++q) {
@@ -849,11 +865,11 @@ struct Stepper {
             // a lagging commitIndex, Q9) the replay below runs.
             const uint64_t hi2 = run & lm(n.mc > C + 1);                 // (the ticking groups' rows)
             uint64_t slow = run & lm(n.mc < mc_old);
-            if (hi2) slow |= lm(__popc(c.gbits(hi2)) >= MAJ);             // wave-uniform, rare
+            if (RARE(hi2)) slow |= lm(__popc(c.gbits(hi2)) >= MAJ);             // wave-uniform, rare
 #ifdef RAFT_EXP_COMMIT_REPLAY
             slow = ~0ull;                                                 // A/B experiment only: always replay
 #endif
-            if (!slow) {
+            if (LIKELY(!slow)) {
                 const uint64_t upto = lm((ck >> c.r) != 0u);              // rows at or before q*
                 const int32_t cur = ib(upto) ? n.mc : mc_old;
                 const uint64_t inc = lm(__popc(c.gbits(lm(cur > C))) >= MAJ) & lm(ck != 0u);   // :161-162
@@ -953,18 +969,21 @@ struct Stepper {
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t mme = lm(r == s);
-        const uint64_t lreq = mine & lost(p, c, s, mme, dw, 0);     // retry{} swallows, Commons.kt:41
+        const uint64_t net = lost_net(c, s);
+        const uint64_t lreq = mine & lost(p, net, mme, dw, 0);      // retry{} swallows, Commons.kt:41
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
         vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, hasl, fs, cnt, rterm, granted);
-        const uint64_t lresp = act & lost(p, c, s, mme, dw, 1);
+        const uint64_t lresp = act & lost(p, net, mme, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
         // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
         const uint32_t dl = c.gbits(delivered);
         const uint32_t gr = c.gbits(delivered & granted);
-        const uint32_t hi = c.gbits(delivered & lm(rterm > st));
+        const uint64_t him = delivered & lm(rterm > st);
+        uint32_t hi = 0;
+        if (RARE(him)) hi = c.gbits(him);                                 // wave-uniform, rare
         const bool me = ib(mvr & mme);
         uint32_t f = n.fl & ~(dl << PEND_SH);
         f += (uint32_t)__popc(dl) << LATCH_SH;                      // :209 countDown()
@@ -974,7 +993,7 @@ struct Stepper {
         if constexpr (TB) {
             // textbook: the candidate adopts the highest response term once its
             // round's responses are in (the reference keeps its term, Q6)
-            if (lm(hi != 0)) {                                      // wave-uniform, rare
+            if (RARE(lm(hi != 0))) {                                      // wave-uniform, rare
                 int32_t T = st;
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
@@ -1182,7 +1201,7 @@ struct Stepper {
             n.retry = ib(dec) ? 0 : n.retry;
             dstart = endel & lm(n.role == RAFT_LEADER);
         }
-        if (need_bo) {
+        if (RARE(need_bo)) {
             const uint32_t w = timer_word(p, c);
             const KernArgs kp = kernargs();
             if (ib(need_bo)) n.phase = scale_range(w, kp->bmin, kp->bmax);
@@ -1197,7 +1216,7 @@ struct Stepper {
         // mt: the lanes of groups with a session left to tick (each round's
         // predicate and the loop condition, one ballot per round)
         uint64_t mt = lm(todo != 0);
-        if (mt) {
+        if (LIKELY(mt)) {
             const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during A
             {
                 // R = 2: the job lanes do not hold the first leader's chunk,
@@ -1209,7 +1228,7 @@ struct Stepper {
                 tick<FIRST_STAGED>(p, c, n, mt, s, fs, cnt);
             }
             mt = lm(todo != 0);
-            if (mt) {                                                       // 2+ sessions (rare)
+            if (RARE(mt)) {                                                 // 2+ sessions (rare)
                 constexpr bool ALL = L::SENDERS_STAGED;
                 if constexpr (ALL && L::TICK_JOB) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
                 do {
@@ -1242,7 +1261,7 @@ struct Stepper {
         {
             cnt.add(isl, RAFT_C_LEADERS);
             cnt.add(lm(lead != 0) & L::lanes_of(0), RAFT_C_GROUPS_WITH_LEADER);   // one lane per group
-            if (lm(__popc(lead) >= 2)) {                                    // rare
+            if (RARE(lm(__popc(lead) >= 2))) {                                    // rare
                 bool dual = false;
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
