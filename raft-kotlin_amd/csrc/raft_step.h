@@ -1054,7 +1054,9 @@ struct Stepper {
             n.voted = bsr ? r + 1 : n.voted;                                // :193
             const uint32_t fr = (f & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
                                 (ALL << PEND_SH) | (ib(start_fire) ? FL_ELECTING : 0u);
-            n.fl = bsr ? fr : (bend ? end_flags(f, n.role) : f);
+            uint32_t fe = f;                                                // the flags of an election that ends
+            if (RARE(endel)) fe = end_flags(f, n.role);                     // (rare: ~9 VALU skipped)
+            n.fl = bsr ? fr : (bend ? fe : f);
             n.phase = (bsr || bend) ? 0 : ph;
             n.retry = (bsr || bend) ? 0 : rty;
             sstart = endel & lm(n.role == RAFT_LEADER);
@@ -1183,25 +1185,34 @@ struct Stepper {
 
         c.clk.mark(PH_V);
         // ---------------- D: latch closes -> decision (RaftServer.kt:214-222) ----------------
-        uint64_t dstart, need_bo;
+        // only waves where some round closes this step do any of it
+        uint64_t dstart = 0, need_bo = 0;
         {
             const uint32_t f = n.fl;
-            const int latch = (f >> LATCH_SH) & 0xF, votes = (f >> VOTES_SH) & 0xF;
-            const uint64_t dec = lm(f & FL_ELECTING) & ~lm(f & FL_BACKOFF) &
-                                 (lm(latch >= MAJ) | lm(n.phase >= p.round_to));
-            const uint64_t cand = dec & lm(n.role == RAFT_CANDIDATE);
-            const uint64_t win = cand & lm(votes >= MAJ);                   // :218-219
-            need_bo = cand & ~win;                                          // :220-221
-            const uint64_t endel = dec & ~need_bo;
-            const uint32_t fc = f & ~(0xFFu << PEND_SH);                    // cancelChildren() :215
-            n.role = ib(win) ? (int32_t)RAFT_LEADER : n.role;
-            const uint32_t fb = (fc & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
-            n.fl = ib(endel) ? end_flags(fc, n.role) : (ib(need_bo) ? fb : f);
-            n.phase = ib(endel) ? 0 : n.phase;
-            n.retry = ib(dec) ? 0 : n.retry;
-            dstart = endel & lm(n.role == RAFT_LEADER);
+            const uint64_t inr = lm(f & FL_ELECTING) & ~lm(f & FL_BACKOFF);     // in a vote round
+            uint64_t dec = 0;
+            if (inr) {                                                      // wave-uniform
+                const int latch = (f >> LATCH_SH) & 0xF;
+                dec = inr & (lm(latch >= MAJ) | lm(n.phase >= p.round_to));
+            }
+            if (dec) {                                                      // wave-uniform
+                const int votes = (f >> VOTES_SH) & 0xF;
+                const uint64_t cand = dec & lm(n.role == RAFT_CANDIDATE);
+                const uint64_t win = cand & lm(votes >= MAJ);               // :218-219
+                need_bo = cand & ~win;                                      // :220-221
+                const uint64_t endel = dec & ~need_bo;
+                const uint32_t fc = f & ~(0xFFu << PEND_SH);                // cancelChildren() :215
+                n.role = ib(win) ? (int32_t)RAFT_LEADER : n.role;
+                const uint32_t fb = (fc & ~((0xFu << VOTES_SH) | (0xFu << LATCH_SH))) | FL_BACKOFF;
+                uint32_t fe = f;
+                if (endel) fe = end_flags(fc, n.role);                      // wave-uniform
+                n.fl = ib(endel) ? fe : (ib(need_bo) ? fb : f);
+                n.phase = ib(endel) ? 0 : n.phase;
+                n.retry = ib(dec) ? 0 : n.retry;
+                dstart = endel & lm(n.role == RAFT_LEADER);
+            }
         }
-        if (RARE(need_bo)) {
+        if (need_bo) {
             const uint32_t w = timer_word(p, c);
             const KernArgs kp = kernargs();
             if (ib(need_bo)) n.phase = scale_range(w, kp->bmin, kp->bmax);
