@@ -594,7 +594,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
             const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, q.term, q.leader_id, pv,
                                                        q.prev_log_term, __ballot(q.has_entry != 0),
                                                        Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
-                                                       __ballot(pv + 1 == x.last), __ballot(pv >= 0), follower_sent(x.fl),
+                                                       __ballot(pv + 1 == x.last), __ballot(pv >= 0),
+                                                       __ballot(q.leader_id != r + 1), follower_sent(x.fl),
                                                        cnt, rt, su, st);
             ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {

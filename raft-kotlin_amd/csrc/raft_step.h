@@ -367,17 +367,19 @@ __device__ __forceinline__ void vote_handler(Rep n, uint64_t act, int32_t id, in
 // entry the request vouches for, and never goes down.
 //
 // CHK: the log is a log_window ring: mask slots, count window misses.
-// at_last = lm(prev + 1 == lastIndex), p0 = lm(prev >= 0): the caller's masks
-// (see log_add); fsent = follower_sent(fl), made once per phase (see vote_handler).
+// at_last = lm(prev + 1 == lastIndex), p0 = lm(prev >= 0), other = lm(rlead != id):
+// the caller's masks (see log_add); fsent = follower_sent(fl), made once per
+// phase (see vote_handler).
 template <bool TB, bool CHK, class CNT>
 __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t id, const LogView& lv, int32_t rt,
                                                    int32_t rlead, int32_t prev, int32_t prevTerm, uint64_t has,
                                                    Entry e, int32_t lcommit, int32_t dprev, int32_t dnext,
-                                                   uint64_t at_last, uint64_t p0, uint32_t fsent, CNT& cnt,
-                                                   int32_t& resp_term, uint64_t& success, uint64_t& stored) {
+                                                   uint64_t at_last, uint64_t p0, uint64_t other, uint32_t fsent,
+                                                   CNT& cnt, int32_t& resp_term, uint64_t& success,
+                                                   uint64_t& stored) {
     if constexpr (TB) act &= ~lm(rt < n.term);
     const uint64_t up = act & lm(rt > n.term);                                  // :257-262
-    const uint64_t fol = up | (act & lm(rlead != id));                          // :264-268 (Q3)
+    const uint64_t fol = up | (act & other);                                    // :264-268 (Q3): rlead != id
     const bool u = ib(up), f = ib(fol);
     n.fl |= f ? fsent : 0u;
     n.term = u ? rt : n.term;
@@ -689,7 +691,8 @@ struct Stepper {
         uint32_t dw;
         if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
         else dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
-        n.fl &= ib(mtk & ~run & mme) ? ~FL_HB : ~0u;                      // :117 cancel() (S-10)
+        const uint64_t cancel = mtk & ~run & mme;                         // :117 cancel() (S-10)
+        if (RARE(cancel)) n.fl &= ib(cancel) ? ~FL_HB : ~0u;
         cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
         const uint64_t swap = run & lm(n.s0 != s);                        // swap the session in (rare)
         if (RARE(swap)) {
@@ -759,7 +762,7 @@ struct Stepper {
         uint64_t succ, stored;
         // no lane of act throws: ok implies prev >= -1
         append_handler<TB, RING>(n.rep(), act, c.r + 1, lv, Lterm, s + 1, prev, lpt, has,
-                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, fs, cnt, rterm, succ,
+                           Entry{(int32_t)lent.x, lent.y}, Lcommit, dpt, dnt, at_last, p0, ~mme, fs, cnt, rterm, succ,
                            stored);
         // TB, ae_max_entries > 1: the request carries kq = min(E, Llast - i + 1)
         // entries (greeter.proto:37); the first went through append_handler, the
@@ -1270,9 +1273,10 @@ struct Stepper {
         c.clk.mark(PH_C);
         // ---------------- K: end-of-step observations ----------------
         {
+            const uint64_t glead = lm(lead != 0) & L::lanes_of(0);         // one lane per group with a leader
             cnt.add(isl, RAFT_C_LEADERS);
-            cnt.add(lm(lead != 0) & L::lanes_of(0), RAFT_C_GROUPS_WITH_LEADER);   // one lane per group
-            if (RARE(lm(__popc(lead) >= 2))) {                                    // rare
+            cnt.add(glead, RAFT_C_GROUPS_WITH_LEADER);
+            if (RARE(__popcll(isl) != __popcll(glead))) {                   // some group has 2+ leaders (rare)
                 bool dual = false;
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
@@ -1286,9 +1290,10 @@ struct Stepper {
 
         c.clk.mark(PH_K);
         // the deferred ResettableCountdownTimer draws of this step (S-9)
-        if (__ballot((n.fl & FL_DRAW) != 0)) {
+        const uint64_t dm = lm(n.fl & FL_DRAW);
+        if (dm) {
             const uint32_t w = timer_word(p, c);
-            if (n.fl & FL_DRAW) {
+            if (ib(dm)) {
                 const KernArgs kp = kernargs();
                 n.elec = scale_range(w, kp->emin, kp->emax);
                 n.fl &= ~FL_DRAW;
