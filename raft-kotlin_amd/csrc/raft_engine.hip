@@ -222,6 +222,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         }
         const KernArgs kp = kernargs();
         const int32_t pperiod = kp->part_period;
+        c.part_me = 0;                                                    // made each step: not loop-carried
         if (pperiod > 0) {                                                // S-11 partitions
             const uint32_t ph = t % (uint32_t)pperiod;
             if ((int64_t)ph < kp->part_len) {
@@ -229,8 +230,8 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
             } else {
                 c.part = 0;
             }
+            c.part_me = lm((c.part >> c.r) & 1u);
         }
-        c.part_me = lm((c.part >> c.r) & 1u);                           // made each step: not loop-carried
         Counters cnt;
         cnt.clear();
         Stepper<R, TB, RING>::step(p, c, n, cnt);

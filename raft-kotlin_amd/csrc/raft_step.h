@@ -562,13 +562,15 @@ __device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const C
     return word_of(w, q & 3);
 }
 
-// Word k of the job that lane job_lane of this lane's group drew, read from
-// the wave's LDS staging (one ds_read_b32 instead of four ds_bpermute and a
-// select).  Dead lanes may address past their wave's rows; their words are
-// never used.
+// Word q of the jobs that this lane's group drew from its job lane first_job
+// on, read from the wave's LDS staging (one ds_read_b32 instead of four
+// ds_bpermute and a select).  The staging is [64 lanes][4 words], so word
+// q & 3 of the job of lane first_job + (q >> 2) is word 4 * first_job + q of
+// the group's rows: no split into lane and word.  Dead lanes may address past
+// their wave's rows; their words are never used.
 template <int R>
-__device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int job_lane, int k) {
-    return c.jl[(c.src(job_lane) << 2) + k];
+__device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int first_job, int q) {
+    return c.jl[((c.base + first_job) << 2) + q];
 }
 
 template <int R, bool HAVE_JOB>
@@ -589,11 +591,11 @@ __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& 
 
 // This lane's word of the drop-word chunks the step's jobs drew for sender s
 // (first_job = J_TICK / J_VOTE).  MUST be called in group-uniform control flow.
+// Word dd = (d < s ? d : d - 1) for destination d = this lane; the sender's
+// own lane (d == s, never lost) reads word d, a valid word it ignores.
 template <int R>
 __device__ __forceinline__ uint32_t job_drop_word(const Ctx<R>& c, int first_job, int s) {
-    const int dd = c.r < s ? c.r : c.r - 1;
-    const int q = dd < 0 ? 0 : dd;
-    return job_word(c, first_job + (q >> 2), q & 3);
+    return job_word(c, first_job, dec_if(c.r, lm(c.r > s)));
 }
 
 // The step's per-replica draw word, word r & 3 of Philox(t, gid, TIMER, r >> 2)
@@ -1117,7 +1119,7 @@ struct Stepper {
             hw1 = h.y;
             hw2 = h.z;
             // every word this lane needs from the jobs, fetched in one batch
-            c.tw = job_word(c, L::J_TIMER + (r >> 2), r & 3);
+            c.tw = job_word(c, L::J_TIMER, r);                              // word r & 3 of timer quad r >> 2
             if constexpr (L::TICK_JOB) c.dwt = job_drop_word(c, L::J_TICK, c.s_tick);
             if constexpr (L::VOTE_JOB) c.dwv = job_drop_word(c, L::J_VOTE, c.s_vote);
         } else {
