@@ -291,8 +291,8 @@ __global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
     p.st[fidx(p, F_T2, idx)] = (int32_t)b.x;
 }
 
-// counters[k][c] = sum over the step workgroups b of the 16-bit half (c & 1)
-// of partials[k][c >> 1][b], in ONE dispatch with no memset (a memset, an
+// counters[k][c] = sum over the step workgroups b of the 16-bit half of
+// partials[k][][b] at COUNTER_SLOT[c] (raft_step.h), in ONE dispatch with no memset (a memset, an
 // atomic-add reduction and their two dependent dispatch gaps were ~6 % of a
 // 20-step run).  Grid (chunks, nsteps * NCW): each workgroup sums both halves
 // of one packed counter word over a chunk of REDUCE_CHUNK partials (each word
@@ -307,7 +307,8 @@ constexpr int ACC_TICKET_SH = 48;
 __device__ __forceinline__ uint32_t part_word(const uint32_t* part, int64_t k, int w, int64_t nparts, int b) {
     return part[(k * NCW + w) * nparts + b];
 }
-__device__ __forceinline__ uint32_t half_of(uint32_t x, int c) { return (x >> (16 * (c & 1))) & 0xFFFFu; }
+// counter c's half of a partial word of its slot
+__device__ __forceinline__ uint32_t half_of(uint32_t x, int c) { return (x >> (16 * (COUNTER_SLOT[c] & 1))) & 0xFFFFu; }
 // One counter's total: a direct store for a one-chunk grid, else the ticketed accumulator.
 __device__ __forceinline__ void reduce_emit(int64_t* row, int c, unsigned long long s, unsigned long long nch,
                                             unsigned long long* acc) {
@@ -327,9 +328,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* 
                                                                 unsigned long long* __restrict__ accum) {
     __shared__ uint32_t acc[2][WAVES_PER_BLOCK];
     const int k = blockIdx.y / NCW, w = blockIdx.y % NCW;
-    const int c0 = 2 * w, c1 = 2 * w + 1;
+    const int c0 = counter_of_slot(2 * w), c1 = counter_of_slot(2 * w + 1);   // -1: an unused slot
     const int b0 = blockIdx.x * REDUCE_CHUNK;
     constexpr int SK = RAFT_C_APPEND_SKIPPED;
+    constexpr int TK = RAFT_C_SESSIONS_TICKED, SN = RAFT_C_APPEND_SENT;
     uint32_t lo = 0, hi = 0;        // < 2^19 * 16 per thread
 #pragma unroll
     for (int i = 0; i < REDUCE_CHUNK / BLOCK; ++i) {      // independent loads
@@ -337,10 +339,9 @@ __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* 
         if (b < nparts) {
             const uint32_t x = part_word(partials, k, w, nparts, b);
             uint32_t d = 0;
-            if (w == SK >> 1)
-                d = (uint32_t)R * half_of(part_word(partials, k, RAFT_C_SESSIONS_TICKED >> 1, nparts, b),
-                                          RAFT_C_SESSIONS_TICKED) -
-                    half_of(part_word(partials, k, RAFT_C_APPEND_SENT >> 1, nparts, b), RAFT_C_APPEND_SENT);
+            if (w == COUNTER_SLOT[SK] >> 1)
+                d = (uint32_t)R * half_of(part_word(partials, k, COUNTER_SLOT[TK] >> 1, nparts, b), TK) -
+                    half_of(part_word(partials, k, COUNTER_SLOT[SN] >> 1, nparts, b), SN);
             lo += c0 == SK ? d : x & 0xFFFFu;
             hi += c1 == SK ? d : x >> 16;
         }
@@ -360,8 +361,8 @@ __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* 
         sh += acc[1][q];
     }
     const unsigned long long nch = gridDim.x;
-    reduce_emit(row, c0, sl, nch, &accum[(int64_t)k * NC + c0]);
-    if (c1 < NC) reduce_emit(row, c1, sh, nch, &accum[(int64_t)k * NC + c1]);
+    if (c0 >= 0) reduce_emit(row, c0, sl, nch, &accum[(int64_t)k * NC + c0]);
+    if (c1 >= 0) reduce_emit(row, c1, sh, nch, &accum[(int64_t)k * NC + c1]);
 }
 
 // canonical export [n][W] of groups [g0, g0+n): one thread per group

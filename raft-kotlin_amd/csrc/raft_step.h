@@ -45,6 +45,26 @@ namespace raft {
 
 constexpr int NC = RAFT_NUM_COUNTERS;
 constexpr int NCW = (NC + 1) / 2;          // counters packed as 16-bit pairs per lane
+// Half-word slot of each counter in the packed rows (slot >> 1: word, slot & 1:
+// half).  The counters added most often per wave-step take the low halves, which
+// need no shift before the add (one SALU fewer per event mask; SALU issue is a
+// bottleneck of the step kernel).  The reduction decodes with counter_of_slot.
+constexpr int COUNTER_SLOT[RAFT_NUM_COUNTERS] = {
+    /* LEADERS            */ 7,  /* GROUPS_WITH_LEADER */ 9,  /* TIMEOUTS           */ 11,
+    /* ROUNDS             */ 13, /* VOTES_GRANTED      */ 6,  /* LEADERS_ELECTED    */ 15,
+    /* SESSIONS_TICKED    */ 8,  /* APPEND_SENT        */ 10, /* APPEND_SKIPPED     */ 21,
+    /* ENTRIES_ACKED      */ 20, /* COMMITS            */ 1,  /* MSG_DROPPED        */ 0,
+    /* COMMANDS           */ 5,  /* COMMIT_REGRESSIONS */ 3,  /* DUAL_LEADER_GROUPS */ 17,
+    /* LOG_OVERFLOW       */ 4,  /* PREV_READS_LEADER  */ 12, /* ENTRY_READS_LEADER */ 14,
+    /* PREV_READS_FOLLOWER*/ 16, /* ENTRY_WRITES       */ 18, /* VOTE_LOG_READS     */ 2,
+    /* LOG_WINDOW_MISS    */ 19,
+};
+static_assert(RAFT_NUM_COUNTERS == 22, "COUNTER_SLOT lists every counter");
+__host__ __device__ constexpr int counter_of_slot(int slot) {
+    for (int c = 0; c < RAFT_NUM_COUNTERS; ++c)
+        if (COUNTER_SLOT[c] == slot) return c;
+    return -1;
+}
 
 // exported flag bits (include/raft_engine.h) and engine-internal ones
 constexpr uint32_t FL_ARMED = RAFT_FL_ARMED;
@@ -172,10 +192,12 @@ struct Counters {
     __device__ __forceinline__ void add(uint64_t, int) {}
 #elif defined(RAFT_EXP_NO_MISS)
     __device__ __forceinline__ void add(uint64_t m, int c) {     // timing experiment only
-        if (c != RAFT_C_LOG_WINDOW_MISS) s[c >> 1] += (uint32_t)__popcll(m) << (16 * (c & 1));
+        if (c != RAFT_C_LOG_WINDOW_MISS) s[COUNTER_SLOT[c] >> 1] += (uint32_t)__popcll(m) << (16 * (COUNTER_SLOT[c] & 1));
     }
 #else
-    __device__ __forceinline__ void add(uint64_t m, int c) { s[c >> 1] += (uint32_t)__popcll(m) << (16 * (c & 1)); }
+    __device__ __forceinline__ void add(uint64_t m, int c) {
+        s[COUNTER_SLOT[c] >> 1] += (uint32_t)__popcll(m) << (16 * (COUNTER_SLOT[c] & 1));
+    }
 #endif
 };
 // The per-message handlers of batch_kernel run in divergent control flow and
