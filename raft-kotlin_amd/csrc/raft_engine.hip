@@ -226,7 +226,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         if (pperiod > 0) {                                                // S-11 partitions
             const uint32_t ph = t % (uint32_t)pperiod;
             if ((int64_t)ph < kp->part_len) {
-                if (k == 0 || ph == 0) c.part = draw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
+                if (k == 0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
             } else {
                 c.part = 0;
             }
@@ -792,6 +792,10 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.nslots = (int32_t)nslots;
     const int64_t log_waves = (G + 64 / R - 1) / (64 / R);           // step-kernel waves: one log block each
     d.key0 = (uint32_t)p->seed; d.key1 = (uint32_t)(p->seed >> 32);
+    for (int i = 0; i < 10; ++i) {                                    // Philox round keys (kdraw)
+        d.rk[2 * i] = d.key0 + (uint32_t)i * 0x9E3779B9u;
+        d.rk[2 * i + 1] = d.key1 + (uint32_t)i * 0xBB67AE85u;
+    }
     d.P = p->heartbeat_ms; d.emin = p->election_min_ms; d.emax = p->election_max_ms;
     d.bmin = p->backoff_min_ms; d.bmax = p->backoff_max_ms; d.round_to = p->round_timeout_ms; d.retry = p->retry_ms;
     d.drop_ppm = p->drop_ppm; d.drop_thr16 = (uint32_t)ppm_thr(p->drop_ppm, 16);

@@ -111,6 +111,7 @@ struct DevParams {
     int32_t churn_steps, part_period, part_len;
     int32_t cmd_mode, cmd_limit;
     int32_t ae_max;                            // entries per AppendEntries request (textbook mode; else 1)
+    uint32_t rk[20];                           // Philox round keys (k0, k1) of rounds 0..9 (kdraw)
 };
 
 struct Entry { int32_t term; uint32_t cmd; };
@@ -142,6 +143,29 @@ __device__ __forceinline__ KernArgs kernargs() {
     KernArgs kp = (KernArgs)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(kp));
     return kp;
+}
+
+// The step kernel's draws (S-9): Philox4x32-10 (philox.h) with the 20 round
+// keys read from the kernarg segment (DevParams::rk, made at create), a few
+// scalar loads per pass instead of 20 s_add (SALU issue is a bottleneck of the
+// step kernel).  The key pointer is opaque per call (kernargs()), so the loads
+// are not hoisted out of the step loop.  Valid only inside step_kernel.
+__device__ __forceinline__ u32x4 kdraw(const DevParams& p, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+#ifdef RAFT_EXP_SALU_KEYS
+    return philox4x32_10(c0, c1, c2, c3, p.key0, p.key1);                  // A/B experiment: keys by s_add
+#else
+    const KernArgs kp = kernargs();
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, kp->rk[2 * i], 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, kp->rk[2 * i + 1], 0x96);
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    return u32x4{c0, c1, c2, c3};
+#endif
 }
 
 // Lane masks.  The step's predicates are built as 64-bit lane masks (SGPR
@@ -580,7 +604,7 @@ __device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const C
 #endif
     const int dd = c.r < s ? c.r : c.r - 1;
     const int q = dd < 0 ? 0 : dd;
-    const u32x4 w = draw(p, c.t, c.gid(), purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
+    const u32x4 w = kdraw(p, c.t, c.gid(), purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
     return word_of(w, q & 3);
 }
 
@@ -629,7 +653,7 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
     if constexpr (Lanes<R>::JOBS) {
         return c.tw;
     } else {
-        return word_of(draw(p, c.t, c.gid(), RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
+        return word_of(kdraw(p, c.t, c.gid(), RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
     }
 }
 
@@ -969,7 +993,7 @@ struct Stepper {
     // wave-uniform control flow.
     __device__ __forceinline__ static void stage_sender_chunks(const DevParams& p, Ctx<R>& c, uint32_t purpose) {
         if (no_drops(p)) return;
-        const u32x4 w = draw(p, c.t, c.gid(), purpose, (uint32_t)c.r);
+        const u32x4 w = kdraw(p, c.t, c.gid(), purpose, (uint32_t)c.r);
         *(uint4*)&c.jl[(c.base + c.r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
         asm volatile("" ::: "memory");
     }
@@ -1129,7 +1153,7 @@ struct Stepper {
             // across the step loop (R = 7 spilled them to scratch)
             asm volatile("" : "+v"(purpose));
 #endif
-            c.job = draw(p, c.t, c.gid(), purpose, sub);
+            c.job = kdraw(p, c.t, c.gid(), purpose, sub);
 #endif
             // stage the wave's jobs in LDS (one ds_write_b128 per lane); a
             // wave's LDS accesses complete in order, so its reads below see
@@ -1145,7 +1169,7 @@ struct Stepper {
             if constexpr (L::TICK_JOB) c.dwt = job_drop_word(c, L::J_TICK, c.s_tick);
             if constexpr (L::VOTE_JOB) c.dwv = job_drop_word(c, L::J_VOTE, c.s_vote);
         } else {
-            const u32x4 h = draw(p, c.t, c.gid(), RAFT_RNG_HARNESS, 0);
+            const u32x4 h = kdraw(p, c.t, c.gid(), RAFT_RNG_HARNESS, 0);
             hw0 = h.x; hw1 = h.y; hw2 = h.z;
         }
 
