@@ -48,6 +48,8 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 constexpr int STEP_BLOCK = RAFT_STEP_BLOCK;
 constexpr int STEP_WAVES = STEP_BLOCK / 64;
 constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
+constexpr int TALLY_LDS_WORDS = STEP_WAVES * 16;          // per-wave vote-tally words (Ctx::tl, R >= 4)
+constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS;
 
 __device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
 
@@ -171,7 +173,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     // LDS: [STEP_WAVES][64][4] the step's Philox job words (Ctx::jl),
     // then the counter rows [nsteps][NCW]
     extern __shared__ uint32_t lds[];
-    uint32_t* const lds_cnt = lds + JOB_LDS_WORDS;
+    uint32_t* const lds_cnt = lds + PRE_CNT_LDS_WORDS;
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
     const int wid = blockIdx.x * STEP_WAVES + wib;
@@ -195,6 +197,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.job = u32x4{0u, 0u, 0u, 0u};
     c.tw = c.dwt = c.dwv = 0u;
     c.jl = lds + wib * 256;
+    c.tl = lds + JOB_LDS_WORDS + wib * 16;
 
     for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
     Node n;
@@ -679,7 +682,7 @@ template <int R> struct InitL {
 };
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1) {
-        const size_t lds = (size_t)(JOB_LDS_WORDS + k * NCW) * 4;
+        const size_t lds = (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4;
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
         auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? (e->p.log_window ? step_kernel<R, true, true> : step_kernel<R, true, false>)
                                                      : (e->p.log_window ? step_kernel<R, false, true> : step_kernel<R, false, false>);

@@ -434,14 +434,16 @@ __device__ __forceinline__ uint64_t append_handler(Rep n, uint64_t act, int32_t 
     if constexpr (!TB) {
         const uint64_t cu = act & lm(lcommit > n.commit);                       // :270-272 (Q4)
         const int32_t cc = min(lcommit, n.last);
-        cnt.add(cu & lm(cc < n.commit), RAFT_C_COMMIT_REGRESSIONS);
+        const uint64_t regr = cu & lm(cc < n.commit);
+        if (RARE(regr)) cnt.add(regr, RAFT_C_COMMIT_REGRESSIONS);
         n.commit = ib(cu) ? cc : n.commit;
     }
-    const uint64_t check = lm(prev != -1) & lm(n.last > prev);                  // :274-276
-    const uint64_t thrown = check & ~p0;
-    cnt.add(act & check & ~thrown, RAFT_C_PREV_READS_FOLLOWER);
-    if constexpr (CHK) cnt.add(act & check & ~thrown & lv.miss(prev, n.phys), RAFT_C_LOG_WINDOW_MISS);   // :276
-    success = act & (lm(prev == -1) | (check & ~thrown & lm(dprev == prevTerm)));
+    const uint64_t lgt = lm(n.last > prev);                                     // :274-276
+    const uint64_t rd = p0 & lgt;                                               // log.get(prev) is read
+    const uint64_t thrown = lm(prev < -1) & lgt;                                // ... and throws (prev < -1)
+    cnt.add(act & rd, RAFT_C_PREV_READS_FOLLOWER);
+    if constexpr (CHK) cnt.add(act & rd & lv.miss(prev, n.phys), RAFT_C_LOG_WINDOW_MISS);   // :276
+    success = act & (lm(prev == -1) | (rd & lm(dprev == prevTerm)));
     uint64_t wrote, ovf, wmiss;
     uint64_t same = 0;                                                          // TB: entry already there
     if constexpr (TB) {
@@ -543,6 +545,7 @@ struct Ctx {
 
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
     uint32_t* jl;             // the wave's LDS staging of the job words, [64 lanes][4]
+    uint32_t* tl;             // the wave's vote-tally words, [16] (one per group at base >> 2, R >= 4)
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
@@ -763,7 +766,7 @@ struct Stepper {
         const uint64_t at_last = lm(prev + 1 == n.last);                  // own log[prev] is the tail (log_add: i == lastIndex)
         const uint64_t ok = run & pge & plt;
         const uint64_t has = pge & lm(i <= Llast);
-        cnt.add(run & p0 & plt, RAFT_C_PREV_READS_LEADER);
+        cnt.add(ok & p0, RAFT_C_PREV_READS_LEADER);                      // ok = run & pge & plt, p0 within pge
         cnt.add(run & has, RAFT_C_ENTRY_READS_LEADER);
         // RAFT_C_APPEND_SKIPPED (run & ~ok) is not counted here: run covers
         // whole groups, so it is R * SESSIONS_TICKED - APPEND_SENT, which the
@@ -1029,16 +1032,38 @@ struct Stepper {
         const uint64_t lresp = act & lost(p, net, mme, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
-        // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
-        const uint32_t dl = c.gbits(delivered);
-        const uint32_t gr = c.gbits(delivered & granted);
         const uint64_t him = delivered & lm(rterm > st);
         uint32_t hi = 0;
         if (RARE(him)) hi = c.gbits(him);                                 // wave-uniform, rare
         const bool me = ib(mvr & mme);
-        uint32_t f = n.fl & ~(dl << PEND_SH);
-        f += (uint32_t)__popc(dl) << LATCH_SH;                      // :209 countDown()
-        f += (uint32_t)__popc(gr) << VOTES_SH;                      // :211
+#ifdef RAFT_EXP_GBITS_TALLY
+        constexpr bool LDS_TALLY = false;                           // A/B experiment only
+#else
+        constexpr bool LDS_TALLY = R >= 4;                          // a word per group at base >> 2
+#endif
+        uint32_t f;
+        if constexpr (LDS_TALLY) {
+            // the sender's tally through LDS (RaftServer.kt:208-212): each
+            // delivered destination d adds one response (:209 countDown()),
+            // its grant (:211) and minus its pending bit (set in the sender's
+            // flags: it was sent to) into its group's word; the sender reads
+            // the sum.  A wave's LDS operations complete in order.
+            // Every lane of a group zeroes its word and adds (0 unless
+            // delivered): no exec-mask changes.
+            uint32_t* const tw = c.tl + (c.base >> 2);                 // one word per group (R >= 4)
+            *tw = 0u;
+            const uint32_t add = (1u << LATCH_SH) + (ib(granted) ? (1u << VOTES_SH) : 0u) - (1u << (PEND_SH + c.r));
+            __hip_atomic_fetch_add(tw, ib(delivered) ? add : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("" ::: "memory");
+            f = n.fl + *tw;
+        } else {
+            // the sender's tally: ballot + popcount (RaftServer.kt:208-212)
+            const uint32_t dl = c.gbits(delivered);
+            const uint32_t gr = c.gbits(delivered & granted);
+            f = n.fl & ~(dl << PEND_SH);
+            f += (uint32_t)__popc(dl) << LATCH_SH;                  // :209 countDown()
+            f += (uint32_t)__popc(gr) << VOTES_SH;                  // :211
+        }
         n.fl = me ? f : n.fl;
         n.role = (me && hi) ? (int32_t)RAFT_FOLLOWER : n.role;     // :210 (Q6)
         if constexpr (TB) {
@@ -1046,6 +1071,7 @@ struct Stepper {
             // round's responses are in (the reference keeps its term, Q6)
             if (RARE(lm(hi != 0))) {                                      // wave-uniform, rare
                 int32_t T = st;
+                const uint32_t dl = c.gbits(delivered);
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
                     const int32_t tq = bcast(rterm, c.src(q));
