@@ -204,6 +204,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     c.clk.start();
     if (live) load_node(n, p, g, idx);
     else inert_node(n);
+    c.lead = c.gbits(__ballot(n.role == RAFT_LEADER));                  // Stepper::step's lead0 of the first step
     // Drain the state loads here: left pending into the loop, they make the
     // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
     // previous step's log stores, so each step would start by waiting for them.

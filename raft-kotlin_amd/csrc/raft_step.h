@@ -546,6 +546,7 @@ struct Ctx {
     u32x4 job;                // this lane's Philox job of the step (Lanes::JOBS), dead after the fetch
     uint32_t* jl;             // the wave's LDS staging of the job words, [64 lanes][4]
     uint32_t* tl;             // the wave's vote-tally words, [16] (one per group at base >> 2, R >= 4)
+    uint32_t lead;            // the group's LEADER bits at the end of the last step (loop-carried)
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
@@ -1091,7 +1092,9 @@ struct Stepper {
         // H needs the roles at step start (the lowest-id LEADER to isolate);
         // T draws no randomness, so it runs before the step's Philox pass and
         // that pass already knows the first RequestVote sender.
-        const uint32_t lead0 = c.gbits(__ballot(n.role == RAFT_LEADER));
+        // the group's LEADER bits at step start: K's of the previous step (no
+        // role changes between K and the next T), made at launch start
+        const uint32_t lead0 = c.lead;
 
         // ---------------- T: timers and election clocks ----------------
         uint32_t send;
@@ -1156,11 +1159,11 @@ struct Stepper {
         // RequestVote sender.  One Philox evaluation of the wave.
         uint32_t hw0, hw1, hw2;
         uint32_t vtodo = c.gbits(__ballot(send != 0));                     // the group's RequestVote senders
-        {
-            const uint32_t hb = c.gbits(__ballot((n.fl & FL_HB) != 0));
-            c.s_tick = hb ? __builtin_ctz(hb) : -1;
-            c.s_vote = vtodo ? __builtin_ctz(vtodo) : -1;
-        }
+        // the group's heartbeat sessions: only D's new leaders add to them
+        // before A (A re-reads them only in a wave where one started)
+        const uint32_t hb = c.gbits(__ballot((n.fl & FL_HB) != 0));
+        c.s_tick = hb ? __builtin_ctz(hb) : -1;
+        c.s_vote = vtodo ? __builtin_ctz(vtodo) : -1;
         if constexpr (L::JOBS) {
             uint32_t purpose = RAFT_RNG_HARNESS, sub = 0;
             if (r >= L::J_TIMER && r < L::J_TICK) {
@@ -1298,7 +1301,8 @@ struct Stepper {
         c.clk.mark(PH_D);
 
         // ---------------- A: leader ticks, senders ascending (S-3, S-4) ----------------
-        uint32_t todo = c.gbits(__ballot((n.fl & FL_HB) != 0));
+        uint32_t todo = hb;
+        if (RARE(dstart)) todo = c.gbits(__ballot((n.fl & FL_HB) != 0));   // D started a session
         // the first round peeled: the common case runs no loop (a loop makes
         // the compiler carry the counters in VGPRs and copy the node per round).
         // mt: the lanes of groups with a session left to tick (each round's
@@ -1347,6 +1351,7 @@ struct Stepper {
         c.clk.mark(PH_C);
         // ---------------- K: end-of-step observations ----------------
         {
+            c.lead = lead;                                                  // the next step's lead0
             const uint64_t glead = lm(lead != 0) & L::lanes_of(0);         // one lane per group with a leader
             cnt.add(isl, RAFT_C_LEADERS);
             cnt.add(glead, RAFT_C_GROUPS_WITH_LEADER);
