@@ -1215,16 +1215,21 @@ struct Stepper {
             // the step they would be spilled into VGPR lanes
             const KernArgs kp = kernargs();
             const uint64_t churn_thr = kp->churn_thr32;
-            const int32_t churn_steps = kp->churn_steps;
-            int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
-            if (rem > 0) { rem--; if (rem == 0) rep = 0; }
-            if (churn_thr && churn_steps > 0 && rem == 0 && hw0 < churn_thr && lead0) {
-                rep = __builtin_ctz(lead0);                                 // lowest-id LEADER
-                rem = churn_steps;
+            c.iso = -1;
+            c.iso_me = 0;
+            // only waves where an isolation runs or may start (~1/5) do the rest
+            if (RARE(lm(n.iso != 0) | lm((uint64_t)hw0 < churn_thr))) {
+                const int32_t churn_steps = kp->churn_steps;
+                int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
+                if (rem > 0) { rem--; if (rem == 0) rep = 0; }
+                if (churn_thr && churn_steps > 0 && rem == 0 && hw0 < churn_thr && lead0) {
+                    rep = __builtin_ctz(lead0);                             // lowest-id LEADER
+                    rem = churn_steps;
+                }
+                n.iso = rem > 0 ? (rem << 8) | rep : 0;
+                c.iso = rem > 0 ? rep : -1;
+                c.iso_me = lm(r == c.iso);
             }
-            n.iso = rem > 0 ? (rem << 8) | rep : 0;
-            c.iso = rem > 0 ? rep : -1;
-            c.iso_me = lm(r == c.iso);
         }
 
         c.clk.mark(PH_H);
