@@ -65,6 +65,12 @@ __host__ __device__ constexpr int counter_of_slot(int slot) {
         if (COUNTER_SLOT[c] == slot) return c;
     return -1;
 }
+constexpr bool counter_slots_are_a_permutation() {
+    for (int q = 0; q < 2 * NCW; ++q)
+        if (q < RAFT_NUM_COUNTERS && counter_of_slot(q) < 0) return false;
+    return true;
+}
+static_assert(counter_slots_are_a_permutation(), "every counter has its own half-word slot");
 
 // exported flag bits (include/raft_engine.h) and engine-internal ones
 constexpr uint32_t FL_ARMED = RAFT_FL_ARMED;
