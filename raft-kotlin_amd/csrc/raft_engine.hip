@@ -213,16 +213,17 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     for (int k = 0; k < nsteps; ++k) {
         const uint32_t t = t0 + (uint32_t)k;
         c.t = t;
-        // Re-derive the lane geometry from the lane id every step, behind an
-        // opaque copy: otherwise the optimiser hoists dozens of loop-invariant
-        // lane masks (r == 1, r < 2, ...) out of the step loop, and each one
-        // pins an SGPR pair for the whole kernel (spilled to VGPR lanes and
-        // reloaded at every use).  r and base are then dead between steps.
+        // The lane geometry (r, base) is carried across steps behind an opaque
+        // copy: otherwise the optimiser hoists dozens of loop-invariant lane
+        // masks (r == 1, r < 2, ...) out of the step loop, and each one pins an
+        // SGPR pair for the whole kernel (spilled to VGPR lanes and reloaded at
+        // every use).  (Round 1 re-derived both from the lane id each step:
+        // 6 VALU more per wave-step and 6 VGPRs more at R = 5, profiles/r2_geom.)
         {
-            int ln = lane;
-            asm volatile("" : "+v"(ln));
-            c.base = (int)(((uint32_t)ln * ((65536u + R - 1) / R)) >> 16) * R;
-            c.r = ln - c.base;
+            int cb = c.base, cr = c.r;
+            asm volatile("" : "+v"(cb), "+v"(cr));
+            c.base = cb;
+            c.r = cr;
         }
         const KernArgs kp = kernargs();
         const int32_t pperiod = kp->part_period;
