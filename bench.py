@@ -226,8 +226,9 @@ def parse_args(argv=None):
                     help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
     ap.add_argument("--ae-max-entries", type=int, default=0,
                     help="textbook mode: entries per AppendEntries request (0/1 = one, the reference's shape)")
-    ap.add_argument("--steps-per-launch", type=int, default=512,
-                    help="upper bound of the lockstep steps fused into one kernel launch (state stays in VGPRs)")
+    ap.add_argument("--steps-per-launch", type=int, default=0,
+                    help="upper bound of the lockstep steps fused into one kernel launch (state stays in VGPRs); "
+                         "0 = the kernel variant's default (abi.bench_steps_per_launch)")
     ap.add_argument("--stream-steps", type=int, default=200,
                     help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
@@ -376,9 +377,10 @@ def main():
         hbm = torch.cuda.get_device_properties(dev).total_memory
         window = 0 if args.config == 5 or flat <= 0.6 * hbm else 256
     log_cap = max(log_cap, window)                          # the window never exceeds the physLen limit
-    L = launch_length(args.steps, args.steps_per_launch)   # every timed launch has L steps
-    chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
     mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
+    spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window)
+    L = launch_length(args.steps, spl)                      # every timed launch has L steps
+    chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
     params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode,
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)

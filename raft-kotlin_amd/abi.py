@@ -43,6 +43,18 @@ COUNTER_NAMES = [
 NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
 MAX_STEPS_PER_LAUNCH = 512
+# bench.py's launch length for the step kernels built for 7 waves per SIMD
+# (reference mode, flat log, R <= 5; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
+# the longest that keeps 7 step workgroups per CU within the LDS (STEP_K_7WG,
+# 433 steps).  The other kernels run 6 workgroups per CU at any length and
+# take the longest launch.
+BENCH_STEPS_PER_LAUNCH = 400
+
+
+def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0) -> int:
+    """Default fused launch length of bench.py for a kernel variant."""
+    seven = mode == MODE_REFERENCE and log_window == 0 and R <= 5
+    return BENCH_STEPS_PER_LAUNCH if seven else MAX_STEPS_PER_LAUNCH
 MAX_AE_ENTRIES = 8           # include/raft_engine.h RAFT_MAX_AE_ENTRIES
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
 

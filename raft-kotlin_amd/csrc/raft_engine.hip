@@ -50,6 +50,10 @@ constexpr int STEP_WAVES = STEP_BLOCK / 64;
 constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
 constexpr int TALLY_LDS_WORDS = STEP_WAVES * 16;          // per-wave vote-tally words (Ctx::tl, R >= 4)
 constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS;
+// the longest launch whose LDS (job rows, tally words, K counter rows) still
+// lets 7 step workgroups share a CU's 160 KB
+constexpr int STEP_K_7WG = (160 * 1024 / 7 / 4 - PRE_CNT_LDS_WORDS) / NCW;
+static_assert(STEP_K_7WG >= 400, "bench.py's launch length (abi.BENCH_STEPS_PER_LAUNCH) keeps 7 workgroups per CU");
 
 __device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
 
@@ -162,11 +166,16 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 // LDS footprint at K * NCW words, so K can reach RAFT_MAX_STEPS_PER_LAUNCH
 // without costing occupancy; the launch's two barriers (zeroing, final copy)
 // sit outside the step loop.
+// Waves per SIMD the register allocation targets: 7 (72 VGPRs, 94 SGPRs)
+// where the kernel fits them without scratch spills (the reference-mode,
+// flat-log kernels at R <= 5), else 6 (80 VGPRs, 106 SGPRs).  Seven
+// workgroups per CU also need the LDS of a launch of at most STEP_K_7WG steps,
+// which bench.py's default launch length respects.
 #ifndef RAFT_STEP_WAVES_PER_EU
-#define RAFT_STEP_WAVES_PER_EU 6   // 80 VGPRs: measured best of 4..8
+#define RAFT_STEP_WAVES_PER_EU(R, TB, RING) ((!(TB) && !(RING) && (R) <= 5) ? 7 : 6)
 #endif
 template <int R, bool TB, bool RING>
-__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU)))
+__global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU(R, TB, RING))))
 void step_kernel(DevParams p, uint32_t t0, int nsteps,
                                                      uint32_t* __restrict__ partials) {
     using L = Lanes<R>;

@@ -16,7 +16,7 @@ TAG=$T/c3 ROUNDS=${ROUNDS:-2} bash scripts/ab.sh || exit $?
 for v in ${VARIANTS:-base}; do
   lib=raft-kotlin_amd/lib/libraft_engine.so; [ "$v" != base ] && lib=raft-kotlin_amd/lib/libraft_engine_$v.so
   RAFT_ENGINE_LIB=$PWD/$lib timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
-      -d "$OUT/sq_$v" -o run --output-format csv -- python bench.py --steps 2048 --warmup 0 --stream-steps 0 \
+      -d "$OUT/sq_$v" -o run --output-format csv -- python bench.py --steps 2048 --steps-per-launch 512 --warmup 0 --stream-steps 0 \
       --no-cpu-baseline > "$OUT/sq_$v.log" 2>&1 || exit $?
   python3 - "$OUT/sq_$v" "$v" >> "$OUT/status.txt" <<'PY'
 import csv, glob, sys, collections

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build tuning variants of the engine next to the real one, for
 # scripts/variant_sweep.sh (RAFT_ENGINE_LIB selects one; experiments only):
-#   scripts/build_variants.sh "w6:-DRAFT_STEP_WAVES_PER_EU=6" "w8:-DRAFT_STEP_WAVES_PER_EU=8"
+#   scripts/build_variants.sh "w6:-DRAFT_STEP_WAVES_PER_EU(R,TB,RING)=6"
 cd "$(dirname "$0")/.."
 for spec in "$@"; do rm -f raft-kotlin_amd/lib/libraft_engine_${spec%%:*}.so; done
 for spec in "$@"; do

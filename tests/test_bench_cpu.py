@@ -16,6 +16,7 @@ BENCH = os.path.join(ROOT, "bench.py")
 spec = importlib.util.spec_from_file_location("bench", BENCH)
 bench = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(bench)
+abi = bench.abi
 
 
 def run(args, **env):
@@ -66,3 +67,15 @@ def test_world_size_mismatch_is_refused():
 
 def test_cpu_share_is_positive():
     assert 1 <= bench.available_cpus() <= (os.cpu_count() or 1)
+
+
+def test_default_launch_length_per_kernel_variant():
+    """7-waves-per-SIMD kernels (reference mode, flat log, R <= 5) launch at most
+    abi.BENCH_STEPS_PER_LAUNCH steps so 7 workgroups fit a CU's LDS; the others
+    take the longest launch (raft_engine.hip RAFT_STEP_WAVES_PER_EU)."""
+    assert abi.bench_steps_per_launch(5) == abi.BENCH_STEPS_PER_LAUNCH == 400
+    assert abi.bench_steps_per_launch(3) == 400
+    assert abi.bench_steps_per_launch(7) == abi.MAX_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(5, abi.MODE_TEXTBOOK) == abi.MAX_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 256) == abi.MAX_STEPS_PER_LAUNCH
+    assert bench.launch_length(10_000, 400) == 400 and bench.launch_length(20, 400) == 20

@@ -157,7 +157,7 @@ def test_steps_per_launch_invariance():
     kw = dict(abi.CONFIGS[3])
     kw.update(G=5000, churn_ppm=10_000)
     digests = []
-    for k in (1, 7, 32, 128, abi.MAX_STEPS_PER_LAUNCH):          # 600 = one full 512-step launch + 88
+    for k in (1, 7, 32, 128, abi.BENCH_STEPS_PER_LAUNCH, abi.MAX_STEPS_PER_LAUNCH):          # 600 = one full 512-step launch + 88
         e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=k, **kw))
         c = e.step(600)
         digests.append((e.digest(), c.tobytes()))
@@ -276,16 +276,16 @@ def test_textbook_multi_entry_kat_on_engine():
 FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_size.json")
 
 
-@pytest.mark.parametrize("spl", [1, abi.MAX_STEPS_PER_LAUNCH])
+@pytest.mark.parametrize("spl", [1, abi.BENCH_STEPS_PER_LAUNCH, abi.MAX_STEPS_PER_LAUNCH])
 @pytest.mark.parametrize("cfg", [3, 5])
 def test_full_size_digest(cfg, spl):
     """The north star's full-size runs, bit-exact: config 3 (10^6 x 5, 10^4
     steps) and config 5 (10^5 x 7, 10^4 steps) on the GPU against the oracle's
     whole-run digest (state, sessions and every physical log slot of every
     group) and its per-step counters, precomputed on the CPU by
-    tests/golden/make_full_size.py.  Run both one step per launch and with the
-    bench's fused 512-step launches (the exact kernel configuration bench.py
-    times)."""
+    tests/golden/make_full_size.py.  Run one step per launch, with the bench's
+    fused launch length (the kernel configuration bench.py times) and with the
+    longest launch."""
     import json
     meta = json.load(open(FULL))[f"c{cfg}"]
     want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))[f"c{cfg}_counters"]
