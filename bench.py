@@ -163,18 +163,16 @@ def load_pmc(key: dict):
     return None
 
 
-# resident wave slots of the step kernel on one MI355X: 256 CUs x 4 SIMDs x 6
-# waves (occupancy set by the LDS of a 512-step launch)
-WAVE_SLOTS = 256 * 4 * 6
-
-
-def grid_fill(G: int, R: int) -> str:
-    """How the step kernel's waves (one per 64 // R groups) fill the chip."""
+def grid_fill(G: int, R: int, L: int, seven: bool) -> str:
+    """How the step kernel's waves (one per 64 // R groups) fill the chip: 7
+    resident waves per SIMD for the 7-wave kernels launched at most
+    STEP_K_7WG steps (abi.bench_steps_per_launch), else 6."""
     waves = -(-G // (64 // R))
-    if waves < WAVE_SLOTS:
-        return (f"{waves} waves < the {WAVE_SLOTS} resident wave slots of one MI355X: the grid cannot fill "
-                f"the chip ({waves / WAVE_SLOTS:.0%} of the slots), so this rate is not the kernel's throughput")
-    return f"{waves} waves = {waves / WAVE_SLOTS:.2f} rounds of the {WAVE_SLOTS} resident wave slots"
+    slots = SIMDS * (7 if seven and L <= abi.BENCH_STEPS_PER_LAUNCH else 6)
+    if waves < slots:
+        return (f"{waves} waves < the {slots} resident wave slots of one MI355X: the grid cannot fill "
+                f"the chip ({waves / slots:.0%} of the slots), so this rate is not the kernel's throughput")
+    return f"{waves} waves = {waves / slots:.2f} rounds of the {slots} resident wave slots"
 
 
 def free_port() -> int:
@@ -567,7 +565,7 @@ def main():
             "log_window": window, "hbm_bytes_engine": eng.device_bytes,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
             "step_waves_per_rank": -(-G_local // (64 // R)),
-            "grid_fill": grid_fill(G_local, R),
+            "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window) < abi.MAX_STEPS_PER_LAUNCH),
             "counter_allreduce_every": chunk if world > 1 else None,
         },
         "roofline": {
