@@ -157,7 +157,9 @@ def test_steps_per_launch_invariance():
     kw = dict(abi.CONFIGS[3])
     kw.update(G=5000, churn_ppm=10_000)
     digests = []
-    for k in (1, 7, 32, 128, abi.BENCH_STEPS_PER_LAUNCH, abi.MAX_STEPS_PER_LAUNCH):          # 600 = one full 512-step launch + 88
+    # 600 = one full 512-step launch + 88; 433 / 434: the longest launch at 7
+    # workgroups per CU and the shortest at 6 (STEP_K_7WG, raft_engine.hip)
+    for k in (1, 7, 32, 128, abi.BENCH_STEPS_PER_LAUNCH, 433, 434, abi.MAX_STEPS_PER_LAUNCH):
         e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=k, **kw))
         c = e.step(600)
         digests.append((e.digest(), c.tobytes()))
