@@ -163,6 +163,29 @@ def load_pmc(key: dict):
     return None
 
 
+def cycle_split(pmc):
+    """The disjoint split of the step kernel's wave cycles from the PMC row
+    (MI355X_MICROARCH.md, SQ block): issuing (SQ_ACTIVE_INST_ANY), parked on
+    s_waitcnt / barrier (SQ_WAIT_ANY) and ready but not issued
+    (SQ_WAIT_INST_ANY); they sum to about SQ_WAVE_CYCLES.  None when the row
+    lacks that pass."""
+    raw = (pmc or {}).get("pmc_raw") or {}
+    need = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+    if not all(raw.get(k) for k in need):
+        return None
+    wc = raw["SQ_WAVE_CYCLES"]
+    out = {"issuing": raw["SQ_ACTIVE_INST_ANY"] / wc, "waitcnt_or_barrier": raw["SQ_WAIT_ANY"] / wc,
+           "ready_not_issued": raw["SQ_WAIT_INST_ANY"] / wc,
+           "sum": (raw["SQ_ACTIVE_INST_ANY"] + raw["SQ_WAIT_ANY"] + raw["SQ_WAIT_INST_ANY"]) / wc}
+    if raw.get("SQ_WAIT_INST_LDS"):
+        out["lds_issue_stall"] = raw["SQ_WAIT_INST_LDS"] / wc
+    for k in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM",
+              "SQ_ACTIVE_INST_MISC", "SQ_INST_CYCLES_SALU"):
+        if raw.get(k):
+            out[k.lower()[3:] + "_per_wave_cycle"] = raw[k] / wc
+    return out
+
+
 def grid_fill(G: int, R: int, L: int, seven: bool) -> str:
     """How the step kernel's waves (one per 64 // R groups) fill the chip: 7
     resident waves per SIMD for the 7-wave kernels launched at most
@@ -323,8 +346,10 @@ def plan_only(args, world, rank):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse_args()
+def main(argv=None, result=None):
+    """The bench.  `result` (a dict, in-process callers such as the GPU tests)
+    receives the output line's object and the raw counter rows."""
+    args = parse_args(argv)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         return spawn_ranks(args.gpus)                 # the parent never touches a GPU
@@ -344,15 +369,21 @@ def main():
     # rehearsal knobs for a one-GPU box (never set by the driver):
     # RAFT_BENCH_BACKEND=gloo with RAFT_BENCH_ONE_DEVICE=1 runs every rank on
     # cuda:0 with gloo collectives, which exercises the N > 1 path end to end
+    # RAFT_BENCH_FORCE_COLLECTIVE=1 runs the collective branch at WORLD_SIZE 1:
+    # a one-rank communicator (RCCL by default), the side-stream counter
+    # all-reduce per chunk and the elapsed / kernel-time reductions, so the
+    # multi-GPU path executes on a one-GPU box (tests/test_gpu_bench.py)
     backend = os.environ.get("RAFT_BENCH_BACKEND", "nccl")
     if os.environ.get("RAFT_BENCH_ONE_DEVICE") == "1":
         local = 0
-    if world > 1:
+    coll = world > 1 or os.environ.get("RAFT_BENCH_FORCE_COLLECTIVE") == "1"
+    if coll:
         torch.cuda.set_device(local)
+        init = {} if world > 1 else {"init_method": f"tcp://127.0.0.1:{free_port()}", "rank": 0, "world_size": 1}
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), **init)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **init)
     dev = torch.device("cuda", local)
 
     eng_mod = importlib.import_module("raft-kotlin_amd.engine")
@@ -384,7 +415,7 @@ def main():
     eng = eng_mod.RaftEngine(params, device=local)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
-    gcounters = torch.zeros_like(counters) if world > 1 else counters
+    gcounters = torch.zeros_like(counters) if coll else counters
     wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
 
     # ---- warmup (untimed) ----
@@ -392,7 +423,7 @@ def main():
         eng.step_async(args.warmup, wcount.data_ptr())
     eng.sync()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if coll:
         dist.barrier()
 
     # ---- timed region ----
@@ -405,15 +436,15 @@ def main():
     # launch, 6 % of the driver's 20-step run)
     plan = [(q, min(chunk, args.steps - q)) for q in range(0, args.steps, chunk)]
     rows = [counters[q].data_ptr() for q, _ in plan]
-    chunk_ev = [torch.cuda.Event() for _ in plan] if world > 1 else []
+    chunk_ev = [torch.cuda.Event() for _ in plan] if coll else []
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if coll:
         dist.barrier()
     t0 = time.perf_counter()
     ev0.record(stream)
     for ci, (done, k) in enumerate(plan):
         eng.step_async(k, rows[ci])
-        if world > 1:
+        if coll:
             # the only collective: the batched per-step counter all-reduce,
             # off the critical path on a side stream (counters never feed
             # back); this rank's own rows stay in `counters`
@@ -425,7 +456,7 @@ def main():
     ev1.record(stream)
     eng.sync()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if coll:
         dist.barrier()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
@@ -434,7 +465,7 @@ def main():
 
     elapsed = max(wall, ev_ms / 1e3)
     kern_avg_ms = kern_ms / max(1, launches)
-    if world > 1:
+    if coll:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -458,6 +489,8 @@ def main():
     achieved_state = bytes_state / kern_s / 1e9 if launches else 0.0
     overflow = int(c_all[:, abi.C_INDEX["log_overflow"]].sum())
     wmiss = int(c_all[:, abi.C_INDEX["log_window_miss"]].sum())
+    wc = wcount.cpu().numpy()[: args.warmup, : abi.NUM_COUNTERS]      # this rank's untimed legs count too
+    bad_untimed = int(wc[:, abi.C_INDEX["log_overflow"]].sum() + wc[:, abi.C_INDEX["log_window_miss"]].sum())
     pmc_key = {"config": args.config, "mode": args.mode, "groups": G_local, "launch_steps": L,
                "warmup": args.warmup, "steps": args.steps, "log_window": window,
                "kernel_src": kernel_source_id()}
@@ -477,14 +510,15 @@ def main():
             "valu_per_simd_cycle": pmc["valu_per_launch"] / (SIMDS * CLOCK_HZ * kern_avg_ms / 1e3),
             "simd_cycles_per_valu": SIMDS * clk * 1e9 * kern_avg_ms / 1e3 / pmc["valu_per_launch"],
             "effective_clock_ghz": clk,
+            "cycle_split": cycle_split(pmc),
             "source": pmc["source"],
             "note": "SQ_INSTS_VALU of this exact launch and kernel build (rocprofv3 --pmc, same workload, launch "
                     "length and kernel sources) / the live average launch time; peak = 1024 SIMDs x 2.4 GHz / 2 "
                     "cycles per wave64 VALU instruction (MI355X_MICROARCH.md), the rate of the cheapest (VOP2) "
-                    "instructions. This kernel's mix is mostly VOP3 compares, lane-mask selects and 64-bit "
-                    "multiplies, measured at 4.1-4.7 cycles each on gfx950 (profiles/r1_v7/ubench, DESIGN.md "
-                    "§5.1); simd_cycles_per_valu at about that cost means the VALU pipe is saturated. The fused "
-                    "kernel is VALU-issue bound: this is its binding roofline",
+                    "instructions; this kernel's mix is mostly VOP3 compares, lane-mask selects and 64-bit "
+                    "multiplies at 4.1-4.7 cycles each (profiles/r1_v7/ubench). cycle_split is the measured, "
+                    "disjoint split of the waves' cycles (SQ_ACTIVE_INST_ANY issuing, SQ_WAIT_ANY parked on "
+                    "s_waitcnt/barrier, SQ_WAIT_INST_ANY ready but not issued; MI355X_MICROARCH.md SQ block)",
         }
 
     # ---- streaming leg (untimed for `value`): one step per launch, so every
@@ -505,6 +539,7 @@ def main():
         s_state = state_crossing_bytes(cs, G_local, R, s_n) / max(1, s_n)
         s_ach = s_bytes / (s_avg / 1e3) / 1e9
         s_pmc = load_pmc(dict(pmc_key, launch_steps=1, leg="streaming", stream_steps=args.stream_steps))
+        bad_untimed += int(cs[:, abi.C_INDEX["log_overflow"]].sum() + cs[:, abi.C_INDEX["log_window_miss"]].sum())
         streaming = {"steps_per_launch": 1, "steps": args.stream_steps, "kernel_avg_ms": s_avg,
                      "alg_bytes_per_launch": s_bytes, "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": s_ach / HBM_PEAK_GBS,
@@ -525,16 +560,17 @@ def main():
     # ---- safety flags (untimed): the run's counter-borne flags plus the
     # Log Matching check over committed prefixes ----
     mism = eng.check_log_matching()
-    if world > 1:
-        t = torch.tensor([mism], dtype=torch.int64, device=dev)
+    if coll:
+        t = torch.tensor([mism, bad_untimed], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
-        mism = int(t.item())
+        mism, bad_untimed = int(t[0].item()), int(t[1].item())
     safety = {
         "log_matching_mismatched_groups": mism,
         "commit_regressions": int(c_all[:, abi.C_INDEX["commit_regressions"]].sum()),
         "dual_leader_group_steps": int(c_all[:, abi.C_INDEX["dual_leader_groups"]].sum()),
         "log_overflow": overflow,
         "log_window_misses": wmiss,
+        "untimed_overflow_or_window_misses": bad_untimed,
         "note": "observations of the reference's protocol (quirks Q4/Q9 do not preserve these "
                 "properties); over the timed steps, Log Matching at the end of the run",
     }
@@ -566,10 +602,11 @@ def main():
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
             "step_waves_per_rank": -(-G_local // (64 // R)),
             "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window) < abi.MAX_STEPS_PER_LAUNCH),
-            "counter_allreduce_every": chunk if world > 1 else None,
+            "counter_allreduce_every": chunk if coll else None,
+            "collective": ({"backend": backend, "ranks": world, "forced_at_one_rank": world == 1} if coll else None),
         },
         "roofline": {
-            "bound": "hbm", "basis": "alg_equiv", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "bound": "alg_equiv", "basis": "alg_equiv", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_frac": traffic / (kern_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None,
             "kernel": f"step_kernel<{R}> x{L} fused steps", "launch_steps": L,
@@ -593,7 +630,7 @@ def main():
                    "note": "the timed region: wall clock between the barriers/syncs (ms_per_step uses the larger "
                            "of wall and the stream events around it), and the summed step-kernel launches; the "
                            "rest is launch latency, the per-launch counter reduction and the final sync"},
-        "valid": overflow == 0 and wmiss == 0,
+        "valid": overflow == 0 and wmiss == 0 and bad_untimed == 0,
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
@@ -602,8 +639,11 @@ def main():
                                            args.warmup + args.steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if result is not None:
+        result.update(out=out, counters_all=c_all, counters_local=c_loc,
+                      warmup_counters=wcount.cpu().numpy()[: args.warmup, : abi.NUM_COUNTERS])
     eng.close()
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
     return 0
 

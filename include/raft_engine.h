@@ -241,9 +241,11 @@ int64_t raft_engine_device_bytes(raft_engine* e); /* HBM owned by the engine */
 /* out: [n][raft_group_words(R)] int32, canonical layout above. */
 int raft_engine_read_state(raft_engine* e, int64_t g0, int64_t n, int32_t* out);
 int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t* in);
-/* terms/cmds: [n][R][log_cap], physical slot j at [j]; slots >= physLen are
- * unspecified, and with a log_window W the slots below physLen - W read as 0
- * and are not written. */
+/* terms/cmds: [n][R][log_cap], physical slot j at [j].  read_log returns the
+ * retained slots [max(0, physLen - W), physLen) and 0 elsewhere.  write_log to
+ * a flat log (log_window 0) stores every slot below log_cap; with a
+ * log_window W it stores only the slots [max(0, physLen - W), physLen) of the
+ * physLen the engine holds at the call, so call write_state first. */
 int raft_engine_read_log(raft_engine* e, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds);
 int raft_engine_write_log(raft_engine* e, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds);
 /* Order-independent 64-bit digest of the full canonical state and the

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import warnings
 
 import numpy as np
 
@@ -161,6 +162,12 @@ def ptr(a: np.ndarray, ctype):
 _lib = None
 
 
+def _missing_entry(name: str):
+    def stub(*_a, **_k):
+        raise RuntimeError(f"{name} is not in this engine build (RAFT_ENGINE_LIB={os.environ.get('RAFT_ENGINE_LIB')})")
+    return stub
+
+
 def load_library(path: str | None = None):
     """Load the HIP engine.  Raises if it is absent: there is no fallback."""
     global _lib
@@ -215,7 +222,11 @@ def load_library(path: str | None = None):
     }
     for name, (res, args) in sig.items():
         if os.environ.get("RAFT_ENGINE_LIB") and not hasattr(lib, name):
-            continue                     # an older experimental build (RAFT_ENGINE_LIB) may lack newer entry points
+            # an older experimental build (RAFT_ENGINE_LIB) may lack newer
+            # entry points: bind a stub that says so when it is called
+            warnings.warn(f"{path or os.environ['RAFT_ENGINE_LIB']}: no {name}; calls to it will raise", stacklevel=2)
+            setattr(lib, name, _missing_entry(name))
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

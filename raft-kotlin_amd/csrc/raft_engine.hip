@@ -250,11 +250,6 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         cnt.clear();
         Stepper<R, TB, RING>::step(p, c, n, cnt);
         c.clk.mark(PH_TDRAW);
-#ifdef RAFT_EXP_NO_FLUSH
-#pragma unroll
-        for (int cw = 0; cw < NCW; ++cw) asm volatile("" :: "s"(cnt.s[cw]));   // timing experiment only
-        continue;
-#endif
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
         for (int cw = 0; cw < NCW; ++cw) v = (uint32_t)raft_writelane((int32_t)cnt.s[cw], cw, (int32_t)v);
@@ -624,8 +619,11 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
 }
 
 // read_log / write_log: the host's [n][R][log_cap] image of groups [g0, g0+n)
-// <-> the slot-major ring; only the retained slots [max(0, physLen - W),
-// physLen) are copied (the rest reads as 0 and is never written).
+// <-> the engine's log rows.  A read copies the retained slots [max(0,
+// physLen - W), physLen) (the rest reads as 0).  A write to a flat log
+// (log_window 0) stores every slot below log_cap, so it does not depend on
+// the physLen in the engine at the time; a write to a ring stores the slots
+// the current physLen retains (write_state first, include/raft_engine.h).
 __global__ __launch_bounds__(BLOCK) void log_image_kernel(DevParams p, int64_t g0, int64_t n, uint2* img, int to_ring) {
     const int64_t total = n * p.R * (int64_t)p.cap;
     for (int64_t k = (int64_t)blockIdx.x * BLOCK + threadIdx.x; k < total; k += (int64_t)gridDim.x * BLOCK) {
@@ -636,7 +634,7 @@ __global__ __launch_bounds__(BLOCK) void log_image_kernel(DevParams p, int64_t g
         const bool in = j >= window_lo(p, phys) && j < phys;
         uint2* slot = log_of(p, idx).at(j);
         if (to_ring) {
-            if (in) *slot = img[k];
+            if (in || p.W == FLAT_W) *slot = img[k];
         } else {
             img[k] = in ? *slot : make_uint2(0u, 0u);
         }
@@ -802,7 +800,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     // physical slot (no wrap: j < log_cap, and no access is ever a miss)
     const int64_t nslots = p->log_window ? p->log_window : p->log_cap;
     d.wmask = p->log_window ? (uint32_t)(p->log_window - 1) : 0xFFFFFFFFu;
-    d.W = p->log_window ? p->log_window : (1 << 30);
+    d.W = p->log_window ? p->log_window : FLAT_W;
     d.nslots = (int32_t)nslots;
     const int64_t log_waves = (G + 64 / R - 1) / (64 / R);           // step-kernel waves: one log block each
     d.key0 = (uint32_t)p->seed; d.key1 = (uint32_t)(p->seed >> 32);

@@ -108,7 +108,7 @@ struct DevParams {
     int64_t G, g0, GR;
     int32_t R, cap;
     uint32_t wmask;                            // slot of physical index j: j & wmask
-    int32_t W;                                 // window: accesses below physLen - W are misses (2^30 if none)
+    int32_t W;                                 // window: accesses below physLen - W are misses (FLAT_W if none)
     int32_t nslots;                            // NW: slots per replica (< 2^23: 32-bit offsets in a block)
     uint32_t key0, key1;
     int32_t P, emin, emax, bmin, bmax, round_to, retry;
@@ -119,6 +119,8 @@ struct DevParams {
     int32_t ae_max;                            // entries per AppendEntries request (textbook mode; else 1)
     uint32_t rk[20];                           // Philox round keys (k0, k1) of rounds 0..9 (kdraw)
 };
+
+constexpr int32_t FLAT_W = 1 << 30;            // DevParams::W of a flat log (log_window 0): nothing is ever below it
 
 struct Entry { int32_t term; uint32_t cmd; };
 
@@ -157,9 +159,6 @@ __device__ __forceinline__ KernArgs kernargs() {
 // step kernel).  The key pointer is opaque per call (kernargs()), so the loads
 // are not hoisted out of the step loop.  Valid only inside step_kernel.
 __device__ __forceinline__ u32x4 kdraw(const DevParams& p, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-#ifdef RAFT_EXP_SALU_KEYS
-    return philox4x32_10(c0, c1, c2, c3, p.key0, p.key1);                  // A/B experiment: keys by s_add
-#else
     const KernArgs kp = kernargs();
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
@@ -171,7 +170,6 @@ __device__ __forceinline__ u32x4 kdraw(const DevParams& p, uint32_t c0, uint32_t
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
     return u32x4{c0, c1, c2, c3};
-#endif
 }
 
 // Lane masks.  The step's predicates are built as 64-bit lane masks (SGPR
@@ -184,13 +182,8 @@ __device__ __forceinline__ u32x4 kdraw(const DevParams& p, uint32_t c0, uint32_t
 __device__ __forceinline__ uint64_t lm(bool cmp) { return __ballot(cmp); }
 // Branch hints for the wave-uniform rare paths: the common path falls through
 // (a taken s_cbranch restarts the wave's instruction fetch).
-#ifdef RAFT_EXP_NO_EXPECT
-#define RARE(x) (x)
-#define LIKELY(x) (x)
-#else
 #define RARE(x) __builtin_expect(!!(x), 0)
 #define LIKELY(x) __builtin_expect(!!(x), 1)
-#endif
 __device__ __forceinline__ bool ib(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 // x + 1 on the lanes of m: one v_addc_co_u32 with the mask as carry-in (the
 // compiler would emit a v_cndmask and a v_add)
@@ -218,17 +211,9 @@ struct Counters {
 #pragma unroll
         for (int i = 0; i < NCW; ++i) s[i] = 0;
     }
-#ifdef RAFT_EXP_NO_COUNTERS
-    __device__ __forceinline__ void add(uint64_t, int) {}
-#elif defined(RAFT_EXP_NO_MISS)
-    __device__ __forceinline__ void add(uint64_t m, int c) {     // timing experiment only
-        if (c != RAFT_C_LOG_WINDOW_MISS) s[COUNTER_SLOT[c] >> 1] += (uint32_t)__popcll(m) << (16 * (COUNTER_SLOT[c] & 1));
-    }
-#else
     __device__ __forceinline__ void add(uint64_t m, int c) {
         s[COUNTER_SLOT[c] >> 1] += (uint32_t)__popcll(m) << (16 * (COUNTER_SLOT[c] & 1));
     }
-#endif
 };
 // The per-message handlers of batch_kernel run in divergent control flow and
 // report no counters.
@@ -621,9 +606,6 @@ __device__ __forceinline__ uint64_t lost(const DevParams& p, uint64_t net, uint6
 // group-uniform control flow.
 template <int R>
 __device__ __forceinline__ uint32_t drop_word_direct(const DevParams& p, const Ctx<R>& c, uint32_t purpose, int s) {
-#ifdef RAFT_EXP_CHEAP_DROP
-    return (c.gid() * 0x9E3779B1u) ^ (c.t * 0x85EBCA6Bu) ^ ((uint32_t)s << 13) ^ ((uint32_t)c.r << 7);
-#endif
     const int dd = c.r < s ? c.r : c.r - 1;
     const int q = dd < 0 ? 0 : dd;
     const u32x4 w = kdraw(p, c.t, c.gid(), purpose, (uint32_t)s | ((uint32_t)(q >> 2) << 8));
@@ -939,9 +921,6 @@ struct Stepper {
             const uint64_t hi2 = run & lm(n.mc > C + 1);                 // (the ticking groups' rows)
             uint64_t slow = run & lm(n.mc < mc_old);
             if (RARE(hi2)) slow |= lm(__popc(c.gbits(hi2)) >= MAJ);             // wave-uniform, rare
-#ifdef RAFT_EXP_COMMIT_REPLAY
-            slow = ~0ull;                                                 // A/B experiment only: always replay
-#endif
             if (LIKELY(!slow)) {
                 const uint64_t upto = lm((ck >> c.r) != 0u);              // rows at or before q*
                 const int32_t cur = ib(upto) ? n.mc : mc_old;
@@ -1055,11 +1034,7 @@ struct Stepper {
         uint32_t hi = 0;
         if (RARE(him)) hi = c.gbits(him);                                 // wave-uniform, rare
         const bool me = ib(mvr & mme);
-#ifdef RAFT_EXP_GBITS_TALLY
-        constexpr bool LDS_TALLY = false;                           // A/B experiment only
-#else
         constexpr bool LDS_TALLY = R >= 4;                          // a word per group at base >> 2
-#endif
         uint32_t f;
         if constexpr (LDS_TALLY) {
             // the sender's tally through LDS (RaftServer.kt:208-212): each
@@ -1201,17 +1176,11 @@ struct Stepper {
             } else if (r >= L::J_VOTE) {
                 purpose = RAFT_RNG_VOTE_DROP; sub = (uint32_t)(c.s_vote & 0xFF) | ((uint32_t)(r - L::J_VOTE) << 8);
             }
-#ifdef RAFT_EXP_CHEAP_JOB
-            c.job = u32x4{c.gid() * 0x9E3779B1u ^ c.t, c.t * 0x85EBCA6Bu ^ sub, purpose ^ c.gid(), c.gid() + c.t};
-#else
-#ifndef RAFT_EXP_CONST_PURPOSE
             // opaque: otherwise the compiler folds the first Philox round for
             // every lane's constant purpose and keeps those products in VGPRs
             // across the step loop (R = 7 spilled them to scratch)
             asm volatile("" : "+v"(purpose));
-#endif
             c.job = kdraw(p, c.t, c.gid(), purpose, sub);
-#endif
             // stage the wave's jobs in LDS (one ds_write_b128 per lane); a
             // wave's LDS accesses complete in order, so its reads below see
             // them, and the previous step's reads were issued before this write
@@ -1230,12 +1199,6 @@ struct Stepper {
             hw0 = h.x; hw1 = h.y; hw2 = h.z;
         }
 
-#ifdef RAFT_EXP_EXTRA_PHILOX
-        {   // timing experiment only: one more Philox pass of the wave
-            const u32x4 x = draw(p, c.t ^ 0x5A5A5A5Au, c.gid(), 77u, (uint32_t)r);
-            cnt.add(lm(x.x == 0x12345678u), RAFT_C_LEADERS);
-        }
-#endif
         c.clk.mark(PH_JOBS);
         // ---------------- H: harness ----------------
         {

@@ -21,12 +21,25 @@ echo "trace" >> "$OUT/status.txt"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python bench.py $A > "$OUT/trace.log" 2>&1 || exit $?
 i=0
+# pass 4 is the disjoint cycle split of MI355X_MICROARCH.md (SQ block):
+# SQ_WAIT_ANY (parked on s_waitcnt / barrier) + SQ_WAIT_INST_ANY (ready, not
+# issued) + SQ_ACTIVE_INST_ANY (issuing) ~= SQ_WAVE_CYCLES.  Pass 5 is optional
+# (names that this rocprofv3 may not list do not stop the script).
 for pmc in "FETCH_SIZE" "WRITE_SIZE" \
-           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU"; do
   i=$((i+1))
   echo "pmc$i $pmc" >> "$OUT/status.txt"
   timeout -s KILL 300 rocprofv3 --pmc $pmc -d "$OUT/pmc$i" -o run --output-format csv -- \
-      python bench.py $A > "$OUT/pmc$i.log" 2>&1 || exit $?
+      python bench.py $A > "$OUT/pmc$i.log" 2>&1
+  rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "pmc$i rc=$rc" >> "$OUT/status.txt"
+    [ $i -le 4 ] && exit $rc
+    rm -rf "$OUT/pmc$i"
+    [ $rc -eq 137 ] || [ $rc -eq 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ] && exit $rc
+  fi
 done
 for c in FETCH_SIZE WRITE_SIZE; do
   echo "calib $c" >> "$OUT/status.txt"

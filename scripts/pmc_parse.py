@@ -90,6 +90,9 @@ def main(d):
             "waves": m.get("SQ_WAVES"), "wave_cycles": m.get("SQ_WAVE_CYCLES"),
             "busy_cycles": m.get("SQ_BUSY_CYCLES"), "active_inst_valu": m.get("SQ_ACTIVE_INST_VALU"),
             "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"), "launches_averaged": len(ix),
+            # every counter of every pass, per launch (the stall split:
+            # SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~= SQ_WAVE_CYCLES)
+            "pmc_raw": {c: v for c, v in sorted(m.items())},
             "trace_avg_ms": mean([tr[i] for i in ix]) if len(tr) == len(seq) else None,
             "effective_clock_ghz": (m["GRBM_GUI_ACTIVE"] / 8 / (mean([tr[i] for i in ix]) / 1e3) / 1e9
                                     if len(tr) == len(seq) and m.get("GRBM_GUI_ACTIVE") else None),
