@@ -250,6 +250,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps-per-launch", type=int, default=0,
                     help="upper bound of the lockstep steps fused into one kernel launch (state stays in VGPRs); "
                          "0 = the kernel variant's default (abi.bench_steps_per_launch)")
+    ap.add_argument("--subranges", type=int, default=0,
+                    help="step-kernel launch sub-ranges, each on its own stream (0 = the engine's automatic choice)")
     ap.add_argument("--stream-steps", type=int, default=200,
                     help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
@@ -410,7 +412,7 @@ def main(argv=None, result=None):
     spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window)
     L = launch_length(args.steps, spl)                      # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
-    params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode,
+    params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=args.subranges,
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
@@ -527,6 +529,7 @@ def main(argv=None, result=None):
     streaming = None
     if args.stream_steps > 0:
         eng.set_steps_per_launch(1)
+        eng.set_subranges(1)                      # one full-grid launch per step
         sc = torch.zeros((args.stream_steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
         eng.set_kernel_timing(True)
         eng.step_async(args.stream_steps, sc.data_ptr())
@@ -600,6 +603,7 @@ def main(argv=None, result=None):
             "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
             "log_window": window, "hbm_bytes_engine": eng.device_bytes,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
+            "subranges": eng.subranges,
             "step_waves_per_rank": -(-G_local // (64 // R)),
             "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window) < abi.MAX_STEPS_PER_LAUNCH),
             "counter_allreduce_every": chunk if coll else None,

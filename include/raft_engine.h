@@ -60,6 +60,7 @@ extern "C" {
 #define RAFT_MAX_R 8
 #define RAFT_MAX_STEPS_PER_LAUNCH 512   /* steps fused into one kernel launch (LDS counter rows) */
 #define RAFT_MAX_AE_ENTRIES 8           /* textbook mode: entries one AppendEntries request carries */
+#define RAFT_MAX_SUBRANGES 4            /* launch sub-ranges (streams) of the step kernel's grid */
 
 /* ---- command-injection modes (harness) ---------------- */
 #define RAFT_CMD_LOWEST_LEADER 0   /* appendCommand on the lowest-id LEADER  */
@@ -117,7 +118,13 @@ typedef struct raft_params {
                                  * (greeter.proto:37 `repeated LogEntry entries`).  0 or 1 = one
                                  * entry, the reference's shape (RaftServer.kt:130-132); at most
                                  * RAFT_MAX_AE_ENTRIES.  Must be 0 or 1 in reference mode.       */
-    int32_t  reserved[4];
+    int32_t  subranges;         /* engine only: the step kernel's workgroups split into this many
+                                 * contiguous ranges, each launched on its own stream, so that one
+                                 * range's last waves overlap another's next launch (a launch
+                                 * boundary otherwise leaves the chip part-empty while its last
+                                 * waves finish).  0 = automatic (raft_engine_subranges reports the
+                                 * choice), 1..RAFT_MAX_SUBRANGES.  Results never depend on it.     */
+    int32_t  reserved[3];
 } raft_params;
 
 /* ---- per-step counters (sum over the engine's groups) ------------------ */
@@ -222,16 +229,21 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
 int raft_engine_sync(raft_engine* e);
 /* hipStream_t of the engine, as void* (for event timing by the caller). */
 void*   raft_engine_stream(raft_engine* e);
-/* Kernel timing: while enabled, every step-kernel launch is bracketed by a
- * pair of HIP events on the engine stream.  raft_engine_kernel_time()
- * synchronises, returns the summed step-kernel milliseconds and launch count
- * since the last call, and resets them. */
+/* Kernel timing: while enabled, every step-kernel launch (of every
+ * sub-range) carries its own start / stop timestamps.  raft_engine_kernel_time()
+ * synchronises and returns, since the last call, the time during which at
+ * least one step kernel ran (the union of the launches' intervals: sub-range
+ * launches overlap) and the number of K-step launches of the whole grid, then
+ * resets both.  With one sub-range the union is the sum of the launches. */
 int raft_engine_set_kernel_timing(raft_engine* e, int enable);
 int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches);
 int64_t raft_engine_step_index(raft_engine* e);   /* steps executed so far */
 /* Steps fused into one kernel launch from now on (0 = 1), at most
  * RAFT_MAX_STEPS_PER_LAUNCH.  Results do not depend on it. */
 int     raft_engine_set_steps_per_launch(raft_engine* e, int32_t k);
+/* Launch sub-ranges from now on (raft_params.subranges; 0 = automatic). */
+int     raft_engine_set_subranges(raft_engine* e, int32_t n);
+int32_t raft_engine_subranges(raft_engine* e);    /* the sub-ranges in use (-1: null engine) */
 /* Set the index of the next step (its Philox counter c0); with write_state
  * this resumes a run exported at any step. */
 int     raft_engine_set_step_index(raft_engine* e, int64_t t);

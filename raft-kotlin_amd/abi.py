@@ -82,7 +82,7 @@ class raft_params(C.Structure):
         ("partition_period", C.c_int32), ("partition_len", C.c_int32),
         ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
         ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("log_window", C.c_int32),
-        ("ae_max_entries", C.c_int32), ("reserved", C.c_int32 * 4),
+        ("ae_max_entries", C.c_int32), ("subranges", C.c_int32), ("reserved", C.c_int32 * 3),
     ]
 
 
@@ -196,6 +196,8 @@ def load_library(path: str | None = None):
         "raft_engine_step_index": (I64, [eng]),
         "raft_engine_set_step_index": (C.c_int, [eng, I64]),
         "raft_engine_set_steps_per_launch": (C.c_int, [eng, I32]),
+        "raft_engine_set_subranges": (C.c_int, [eng, I32]),
+        "raft_engine_subranges": (I32, [eng]),
         "raft_engine_device_bytes": (I64, [eng]),
         "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
         "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
@@ -240,6 +242,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
+    "raft_engine_set_subranges", "raft_engine_subranges",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",

@@ -161,8 +161,10 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 // K lockstep steps of every group.  A wave holds GPW whole groups, one lane
 // per replica.  Counters: a wave's totals of a step (SGPRs) are added into the
 // workgroup's LDS row [k][NCW] with one return-less ds_add (no wait in the
-// step loop), and after the loop the workgroup copies its rows into the
-// partials [k][NCW][nblocks].  One row per workgroup (not per wave) keeps the
+// step loop), and after the loop the workgroup copies its rows into column
+// part_col0 + blockIdx.x of the partials [k][NCW][part_stride = all step
+// workgroups of the engine].  A launch may cover a sub-range of the waves
+// (wave0 on): the engine's sub-range streams, raft_engine_step_async.  One row per workgroup (not per wave) keeps the
 // LDS footprint at K * NCW words, so K can reach RAFT_MAX_STEPS_PER_LAUNCH
 // without costing occupancy; the launch's two barriers (zeroing, final copy)
 // sit outside the step loop.
@@ -176,8 +178,7 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 #endif
 template <int R, bool TB, bool RING>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU(R, TB, RING))))
-void step_kernel(DevParams p, uint32_t t0, int nsteps,
-                                                     uint32_t* __restrict__ partials) {
+void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     using L = Lanes<R>;
     // LDS: [STEP_WAVES][64][4] the step's Philox job words (Ctx::jl),
     // then the counter rows [nsteps][NCW]
@@ -185,7 +186,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
     uint32_t* const lds_cnt = lds + PRE_CNT_LDS_WORDS;
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    const int wid = blockIdx.x * STEP_WAVES + wib;
+    const int wid = p.wave0 + blockIdx.x * STEP_WAVES + wib;              // wave0: this launch's sub-range
     const int j = lane / R;
     const int r = lane - j * R;
     const int64_t g = (int64_t)wid * L::GPW + j;
@@ -261,8 +262,13 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps,
         c.clk.mark(PH_CNT);
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK)               // workgroup partials
-        partials[(int64_t)q * gridDim.x + blockIdx.x] = lds_cnt[q];
+    {   // workgroup partials; the launch's partials geometry re-read from the
+        // kernarg segment (held across the step loop it would pin SGPRs)
+        const KernArgs kp = kernargs();
+        uint32_t* const part = kp->part + kp->part_col0 + blockIdx.x;
+        const int64_t stride = kp->part_stride;
+        for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) part[(int64_t)q * stride] = lds_cnt[q];
+    }
 #ifdef RAFT_PROFILE_PHASES
     if (lane == 0)
         for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
@@ -656,16 +662,26 @@ struct raft_engine {
     uint64_t t;
     int K;                      // steps per launch
     int nblocks;                // step-kernel workgroups: ceil(G / (STEP_WAVES * (64 / R)))
-    uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials
+    uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials (buffer 0)
+    uint32_t* partials2;        // buffer 1: launches alternate between the two when nsub > 1
+    // launch sub-ranges (raft_engine_step_async): the step workgroups split
+    // into nsub contiguous ranges, each launched on its own stream, so one
+    // range's last waves overlap another's next launch instead of leaving
+    // the chip part-empty at every launch boundary
+    int nsub;
+    int sub_b0[RAFT_MAX_SUBRANGES + 1];       // workgroup boundaries
+    hipStream_t sub_stream[RAFT_MAX_SUBRANGES];
+    hipEvent_t ev_fork, ev_sub_done[RAFT_MAX_SUBRANGES], ev_red_done[2];
+    uint64_t launches_issued;   // step launches (all sub-ranges) so far: the partials buffer parity
     int64_t* counters_dev;      // [K][STRIDE] scratch
     int nchunks;                // counter-reduction chunks of REDUCE_CHUNK partials
     unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
     // step-kernel event timing
     bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
     bool timing;
-    std::vector<hipEvent_t> ev;  // pool, pairs
+    std::vector<hipEvent_t> ev;  // pool, pairs (one per sub-range launch)
     size_t ev_used;
-    int64_t timed_launches;
+    int64_t timed_launches;     // K-step launches of the whole grid timed since the last kernel_time()
 };
 
 template <template <int> class Fn, typename... A>
@@ -690,15 +706,20 @@ template <int R> struct InitL {
     }
 };
 template <int R> struct StepL {
-    static void run(raft_engine* e, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1) {
+    static void run(raft_engine* e, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st, int b0, int b1,
+                    uint32_t* partials) {
         const size_t lds = (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4;
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
         auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? (e->p.log_window ? step_kernel<R, true, true> : step_kernel<R, true, false>)
                                                      : (e->p.log_window ? step_kernel<R, false, true> : step_kernel<R, false, false>);
         // the launch's own start / stop timestamps (ev0, ev1 nullable): no
         // marker packets around the dispatch
-        hipExtLaunchKernelGGL(kern, dim3(e->nblocks), dim3(STEP_BLOCK), (uint32_t)lds, e->stream, ev0, ev1, 0u,
-                              e->dp, t0, k, e->partials);
+        DevParams d = e->dp;
+        d.part = partials;
+        d.wave0 = b0 * STEP_WAVES;
+        d.part_col0 = b0;
+        d.part_stride = e->nblocks;
+        hipExtLaunchKernelGGL(kern, dim3(b1 - b0), dim3(STEP_BLOCK), (uint32_t)lds, st, ev0, ev1, 0u, d, t0, k);
     }
 };
 template <int R> struct PackL {
@@ -778,6 +799,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     if (p->ae_max_entries < 0 || p->ae_max_entries > RAFT_MAX_AE_ENTRIES ||
         (p->mode != RAFT_MODE_TEXTBOOK && p->ae_max_entries > 1))
         return fail(RAFT_EINVAL, "ae_max_entries must be 0..RAFT_MAX_AE_ENTRIES, and 0 or 1 in reference mode");
+    if (p->subranges < 0 || p->subranges > RAFT_MAX_SUBRANGES)
+        return fail(RAFT_EINVAL, "subranges must be 0..RAFT_MAX_SUBRANGES");
     if ((p->log_window ? p->log_window : p->log_cap) >= (1 << 23))
         return fail(RAFT_EINVAL, "log slots per replica (log_window, else log_cap) must be < 2^23");
     int ndev = 0;
@@ -791,6 +814,11 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->cache_valid = true;
     e->ev_used = 0;
     e->timed_launches = 0;
+    e->nsub = 1;
+    e->launches_issued = 0;
+    e->ev_fork = nullptr;
+    for (int q = 0; q < RAFT_MAX_SUBRANGES; ++q) { e->sub_stream[q] = nullptr; e->ev_sub_done[q] = nullptr; }
+    e->ev_red_done[0] = e->ev_red_done[1] = nullptr;
     e->device = device;
     e->t = 0;
     const int64_t G = p->G, R = p->R;
@@ -831,7 +859,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t cnt_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * RAFT_COUNTER_STRIDE * 8;
     e->nchunks = (e->nblocks + REDUCE_CHUNK - 1) / REDUCE_CHUNK;
     const size_t acc_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NC * 8;
-    e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
+    e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + 2 * al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (err != hipSuccess) { delete e; return fail(RAFT_EDEVICE, "hipStreamCreate failed"); }
     err = hipMalloc(&e->base, e->bytes);
@@ -846,10 +874,16 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.spill = (int32_t*)b; b += al(spill_b);
     d.gx = (int32_t*)b; b += al(gx_b);
     e->partials = (uint32_t*)b; b += al(part_b);
+    e->partials2 = (uint32_t*)b; b += al(part_b);
     e->counters_dev = (int64_t*)b; b += al(cnt_b);
     e->accum = (unsigned long long*)b; b += al(acc_b);
     d.log = (uint2*)b;
     *out = e;
+    if (int rc = raft_engine_set_subranges(e, p->subranges)) {
+        raft_engine_destroy(e);
+        *out = nullptr;
+        return rc;
+    }
     dispatch_R<InitL>(p->R, e);
     err = hipMemsetAsync(e->accum, 0, acc_b, e->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
@@ -883,6 +917,12 @@ int raft_engine_destroy(raft_engine* e) {
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->stream);
     for (hipEvent_t x : e->ev) (void)hipEventDestroy(x);
+    for (int q = 0; q < RAFT_MAX_SUBRANGES; ++q) {
+        if (e->sub_stream[q]) (void)hipStreamDestroy(e->sub_stream[q]);
+        if (e->ev_sub_done[q]) (void)hipEventDestroy(e->ev_sub_done[q]);
+    }
+    for (hipEvent_t x : {e->ev_fork, e->ev_red_done[0], e->ev_red_done[1]})
+        if (x) (void)hipEventDestroy(x);
     (void)hipFree(e->base);
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -908,20 +948,48 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
         rebuild_cache_kernel<<<(unsigned)((e->dp.GR + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp);
         e->cache_valid = true;
     }
+    // One sub-range: every launch and its counter reduction on the engine
+    // stream.  nsub > 1: launch k of sub-range q runs on sub_stream[q] and
+    // writes its workgroups' columns of partials buffer k & 1; the engine
+    // stream waits for launch k of every sub-range, reduces that buffer and
+    // marks it free (ev_red_done), which launch k + 2 of each sub-range
+    // waits for.  A sub-range thus runs up to a launch ahead of another, and
+    // its launches follow each other without waiting for the other ranges'
+    // tails.  Work enqueued on the engine stream after this call sees every
+    // launch finished (the last reductions wait for all of them).
+    const bool split = e->nsub > 1;
+    if (split && n_steps > 0) {
+        HIP_TRY(hipEventRecord(e->ev_fork, e->stream));
+        for (int q = 0; q < e->nsub; ++q) HIP_TRY(hipStreamWaitEvent(e->sub_stream[q], e->ev_fork, 0));
+    }
     for (int32_t done = 0; done < n_steps;) {
         const int k = std::min<int32_t>(e->K, n_steps - done);
-        hipEvent_t ev0 = nullptr, ev1 = nullptr;
-        if (e->timing) {
-            if (e->ev_used + 2 > e->ev.size())
-                if (int rc = reserve_events(e, 64)) return rc;
-            ev0 = e->ev[e->ev_used];
-            ev1 = e->ev[e->ev_used + 1];
-            e->ev_used += 2;
+        const int buf = split ? (int)(e->launches_issued & 1) : 0;
+        uint32_t* part = buf ? e->partials2 : e->partials;
+        if (e->timing && e->ev_used + 2 * e->nsub > e->ev.size())
+            if (int rc = reserve_events(e, 64 + e->nsub)) return rc;
+        for (int q = 0; q < e->nsub; ++q) {
+            hipEvent_t ev0 = nullptr, ev1 = nullptr;
+            if (e->timing) {
+                ev0 = e->ev[e->ev_used];
+                ev1 = e->ev[e->ev_used + 1];
+                e->ev_used += 2;
+            }
+            hipStream_t st = split ? e->sub_stream[q] : e->stream;
+            if (split && e->launches_issued >= 2) HIP_TRY(hipStreamWaitEvent(st, e->ev_red_done[buf], 0));
+            dispatch_R<StepL>(e->p.R, e, (uint32_t)(e->t + done), k, ev0, ev1, st, e->sub_b0[q], e->sub_b0[q + 1],
+                              part);
+            if (split) {
+                HIP_TRY(hipEventRecord(e->ev_sub_done[q], st));
+                HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_sub_done[q], 0));
+            }
         }
-        dispatch_R<StepL>(e->p.R, e, (uint32_t)(e->t + done), k, ev0, ev1);
+        if (e->timing) ++e->timed_launches;
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
         const dim3 rg((unsigned)e->nchunks, (unsigned)(k * NCW));
-        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(e->partials, e->nblocks, e->p.R, dst, e->accum);
+        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(part, e->nblocks, e->p.R, dst, e->accum);
+        if (split) HIP_TRY(hipEventRecord(e->ev_red_done[buf], e->stream));
+        ++e->launches_issued;
         done += k;
     }
     HIP_TRY(hipGetLastError());
@@ -967,15 +1035,31 @@ int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches)
     if (!e || !total_ms || !launches) return fail(RAFT_EINVAL, "null argument");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    double acc = 0.0;
+    // intervals relative to the first launch's start, merged: the time during
+    // which at least one step kernel ran (sub-range launches overlap)
+    std::vector<std::pair<double, double>> iv;
     for (size_t q = 0; q + 1 < e->ev_used; q += 2) {
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, e->ev[q], e->ev[q + 1]));
-        acc += ms;
+        float a = 0.f, b = 0.f;
+        if (q) HIP_TRY(hipEventElapsedTime(&a, e->ev[0], e->ev[q]));
+        HIP_TRY(hipEventElapsedTime(&b, e->ev[0], e->ev[q + 1]));
+        iv.emplace_back(a, b);
     }
+    std::sort(iv.begin(), iv.end());
+    double acc = 0.0, lo = 0.0, hi = -1.0;
+    for (const auto& x : iv) {
+        if (x.first > hi) {
+            if (hi > lo) acc += hi - lo;
+            lo = x.first;
+            hi = x.second;
+        } else {
+            hi = std::max(hi, x.second);
+        }
+    }
+    if (hi > lo) acc += hi - lo;
     *total_ms = acc;
-    *launches = (int64_t)(e->ev_used / 2);
+    *launches = e->timed_launches;
     e->ev_used = 0;
+    e->timed_launches = 0;
     return RAFT_OK;
 }
 int64_t raft_engine_step_index(raft_engine* e) { return e ? (int64_t)e->t : -1; }
@@ -985,6 +1069,29 @@ int raft_engine_set_steps_per_launch(raft_engine* e, int32_t k) {
     e->K = k > 0 ? k : 1;
     return RAFT_OK;
 }
+// Sub-ranges: contiguous workgroup ranges of (nearly) equal size.  Automatic
+// (n = 0): one range (see DESIGN.md §6 for the measurements behind the rule).
+int raft_engine_set_subranges(raft_engine* e, int32_t n) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (n < 0 || n > RAFT_MAX_SUBRANGES) return fail(RAFT_EINVAL, "subranges must be 0..RAFT_MAX_SUBRANGES");
+    if (n == 0) n = 1;
+    n = std::min(n, e->nblocks);
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (n > 1 && !e->ev_fork) {
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+        for (int b = 0; b < 2; ++b) HIP_TRY(hipEventCreateWithFlags(&e->ev_red_done[b], hipEventDisableTiming));
+    }
+    for (int q = 0; q < n && n > 1; ++q) {
+        if (!e->sub_stream[q]) HIP_TRY(hipStreamCreateWithFlags(&e->sub_stream[q], hipStreamNonBlocking));
+        if (!e->ev_sub_done[q]) HIP_TRY(hipEventCreateWithFlags(&e->ev_sub_done[q], hipEventDisableTiming));
+    }
+    e->nsub = n;
+    for (int q = 0; q <= n; ++q) e->sub_b0[q] = (int)((int64_t)e->nblocks * q / n);
+    e->launches_issued = 0;              // both partials buffers are free (the engine stream is idle)
+    return RAFT_OK;
+}
+int32_t raft_engine_subranges(raft_engine* e) { return e ? e->nsub : -1; }
 int raft_engine_set_step_index(raft_engine* e, int64_t t) {
     if (!e || t < 0 || t > (int64_t)0xFFFFFFFFll) return fail(RAFT_EINVAL, "bad step index");
     e->t = (uint64_t)t;

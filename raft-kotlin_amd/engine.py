@@ -78,6 +78,15 @@ class RaftEngine:
         self._check(self._lib.raft_engine_set_steps_per_launch(self._h, int(k)), "set_steps_per_launch")
 
     @property
+    def subranges(self) -> int:
+        """Launch sub-ranges in use (raft_params.subranges; streams per launch)."""
+        return int(self._lib.raft_engine_subranges(self._h))
+
+    def set_subranges(self, n: int):
+        """Split the step launches over n sub-range streams (0 = automatic)."""
+        self._check(self._lib.raft_engine_set_subranges(self._h, int(n)), "set_subranges")
+
+    @property
     def device_bytes(self) -> int:
         return int(self._lib.raft_engine_device_bytes(self._h))
 

@@ -172,6 +172,37 @@ def test_steps_per_launch_invariance():
     assert all(d == digests[0] for d in digests)
 
 
+def test_subrange_invariance():
+    """Launch sub-ranges (raft_params.subranges: the grid split over 1-4
+    streams, launches of different ranges overlapping, counter partials
+    double-buffered) change nothing: per-step counters and the digest equal
+    the one-range run at every launch length, also when the count changes
+    mid-run and with kernel timing on."""
+    kw = dict(abi.CONFIGS[3])
+    kw.update(G=7000, churn_ppm=10_000)
+    ref = None
+    for k in (1, 37, abi.BENCH_STEPS_PER_LAUNCH):
+        for n in (1, 2, 3, 4):
+            e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=k, subranges=n, **kw))
+            assert e.subranges == n
+            e.set_kernel_timing(n == 3)
+            c = e.step(600)
+            if n == 3:
+                ms, launches = e.kernel_time()
+                assert launches == -(-600 // k) and ms > 0
+            got = (e.digest(), c.tobytes())
+            ref = ref or got
+            assert got == ref, f"steps_per_launch {k}, {n} sub-ranges"
+            e.close()
+    e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=64, subranges=2, **kw))
+    c1 = e.step(250)
+    e.set_subranges(4)
+    c2 = e.step(200)
+    e.set_subranges(1)
+    c3 = e.step(150)
+    assert (e.digest(), np.concatenate([c1, c2, c3]).tobytes()) == ref
+
+
 def test_shard_invariance():
     """Config 4's contract: sharding by global group id does not change any group."""
     kw = dict(abi.CONFIGS[3])
@@ -284,16 +315,21 @@ FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_
 # driver's `--steps 20` command; the 256-slot ring is step_kernel<5, false,
 # true> (6 waves).  Config 5 is always flat; bench.py launches it at K = 500
 # (launch_length(10^4, 512)).
+# A fourth element is the launch sub-ranges (streams); default 1.
 FULL_SIZE_CASES = [
-    (3, 0, 1), (3, 0, 20), (3, 0, abi.BENCH_STEPS_PER_LAUNCH),
+    (3, 0, 1), (3, 0, 20), (3, 0, abi.BENCH_STEPS_PER_LAUNCH), (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3),
     (3, 256, 1), (3, 256, abi.BENCH_STEPS_PER_LAUNCH), (3, 256, abi.MAX_STEPS_PER_LAUNCH),
-    (5, 0, 1), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH),
+    (5, 0, 1), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH), (5, 0, 500, 2),
 ]
 
 
-@pytest.mark.parametrize("cfg,window,spl", FULL_SIZE_CASES,
-                         ids=[f"{c}-{'flat' if w == 0 else f'ring{w}'}-{k}" for c, w, k in FULL_SIZE_CASES])
-def test_full_size_digest(cfg, window, spl):
+def _full_id(case):
+    c, w, k = case[:3]
+    return f"{c}-{'flat' if w == 0 else f'ring{w}'}-{k}" + (f"-sub{case[3]}" if len(case) > 3 else "")
+
+
+@pytest.mark.parametrize("case", FULL_SIZE_CASES, ids=[_full_id(c) for c in FULL_SIZE_CASES])
+def test_full_size_digest(case):
     """The north star's full-size runs, bit-exact: config 3 (10^6 x 5, 10^4
     steps) and config 5 (10^5 x 7, 10^4 steps) on the GPU against the oracle's
     whole-run digest (state, sessions and every retained log slot of every
@@ -304,11 +340,14 @@ def test_full_size_digest(cfg, window, spl):
     default (400) and one step per launch; the ring cases check the 256-slot
     window (`digest`: the retained slots only)."""
     import json
+    cfg, window, spl = case[:3]
+    nsub = case[3] if len(case) > 3 else 1
     meta = json.load(open(FULL))[f"c{cfg}"]
     want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))[f"c{cfg}_counters"]
     kw = dict(abi.CONFIGS[cfg])
     assert meta["groups"] == kw["G"] and meta["params"] == {k: v for k, v in kw.items() if k != "G"}
-    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], log_window=window, steps_per_launch=spl, **kw))
+    e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], log_window=window, steps_per_launch=spl,
+                                   subranges=nsub, **kw))
     try:
         ce = e.step(meta["steps"])
         if not np.array_equal(ce, want):
