@@ -291,6 +291,18 @@ int raft_append_batch(raft_engine* e, const int64_t* group, const int32_t* dst,
 /* appendCommand (RaftServer.kt:100-107): log.add(lastIndex, (currentTerm, cmd)). */
 int raft_append_command_batch(raft_engine* e, const int64_t* group, const int32_t* replica,
                               const uint32_t* cmd, int64_t n);
+/* The same three on DEVICE buffers of this engine's GPU (group, dst/replica,
+ * req, resp: n entries each, in HBM), enqueued on the engine stream; they
+ * return once the batch finished.  The host entry points above stage their
+ * buffers through engine-owned pinned memory and call these.  A message whose
+ * group or replica is outside the engine makes the whole batch fail with
+ * RAFT_ERANGE before any message is applied.  n < 2^31. */
+int raft_vote_batch_dev(raft_engine* e, const int64_t* group, const int32_t* dst,
+                        const raft_vote_req* req, raft_vote_resp* resp, int64_t n);
+int raft_append_batch_dev(raft_engine* e, const int64_t* group, const int32_t* dst,
+                          const raft_append_req* req, raft_append_resp* resp, int64_t n);
+int raft_append_command_batch_dev(raft_engine* e, const int64_t* group, const int32_t* replica,
+                                  const uint32_t* cmd, int64_t n);
 
 /* ---- Philox4x32-10 (shared bit-for-bit with the CPU harness) -----------
  * Counter = (c0 = step, c1 = global group id, c2 = purpose, c3 = sub),

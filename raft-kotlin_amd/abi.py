@@ -209,6 +209,9 @@ def load_library(path: str | None = None):
         "raft_vote_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_vote_req), P(raft_vote_resp), I64]),
         "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
         "raft_append_command_batch": (C.c_int, [eng, P(I64), P(I32), P(C.c_uint32), I64]),
+        "raft_vote_batch_dev": (C.c_int, [eng, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, I64]),
+        "raft_append_batch_dev": (C.c_int, [eng, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, I64]),
+        "raft_append_command_batch_dev": (C.c_int, [eng, C.c_void_p, C.c_void_p, C.c_void_p, I64]),
         "raft_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
         # include/raft_wire.h
         "raft_wire_decode_vote_req": (C.c_int, [P(C.c_uint8), P(I64), I64, P(raft_vote_req)]),
@@ -246,7 +249,8 @@ EXPORTED_SYMBOLS = [
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
-    "raft_append_command_batch", "raft_philox4x32_10",
+    "raft_append_command_batch", "raft_vote_batch_dev", "raft_append_batch_dev", "raft_append_command_batch_dev",
+    "raft_philox4x32_10",
     # include/raft_wire.h
     "raft_wire_decode_vote_req", "raft_wire_encode_vote_req", "raft_wire_decode_vote_resp",
     "raft_wire_encode_vote_resp", "raft_wire_decode_append_req", "raft_wire_encode_append_req",

@@ -8,6 +8,7 @@
 // handlers read or write, and (rarely) non-primary session rows.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -574,25 +575,51 @@ struct BatchCounters {
     }
 };
 
-// keys[k] = group * R + replica; msgs of key k are order[off[k] .. off[k+1])
+// The batch path on the device (raft_*_batch, raft_*_batch_dev).  Messages
+// to one (group, replica) must be applied in batch order, and messages to
+// different replicas are independent.  batch_keys_kernel turns each message
+// into its key g * R + d (a message outside the engine sets flags[0]); a
+// stable radix sort of (key, message index) then puts each replica's messages
+// next to each other in batch order, and batch_kernel runs one thread per
+// sorted position: the first position of each key's run loads that replica,
+// applies the run's messages in order and stores it back.
+__global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __restrict__ group,
+                                                           const int32_t* __restrict__ dst, int n, int64_t G, int R,
+                                                           uint64_t* __restrict__ keys, uint32_t* __restrict__ ord,
+                                                           unsigned int* flags) {
+    const int m = blockIdx.x * BLOCK + threadIdx.x;
+    if (m >= n) return;
+    const int64_t g = group[m];
+    const int32_t d = dst[m];
+    const bool ok = g >= 0 && g < G && d >= 0 && d < R;
+    keys[m] = ok ? (uint64_t)g * (uint64_t)R + (uint64_t)d : 0ull;
+    ord[m] = (uint32_t)m;
+    if (!ok) atomicOr(&flags[0], 1u);
+}
+
+// flags[0]: a message was outside the engine (nothing is applied);
+// flags[1]: accesses below the retained log window (RAFT_EWINDOW)
 template <bool TB>
-__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int nkeys,
-                                                      const int64_t* keys, const int64_t* off, const int64_t* order,
-                                                      const void* req, void* resp, unsigned int* misses) {
-    const int k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= nkeys) return;
+__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int n,
+                                                      const uint64_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ order, const void* req, void* resp,
+                                                      unsigned int* flags) {
+    const int m0 = blockIdx.x * BLOCK + threadIdx.x;
+    if (m0 >= n || *(volatile unsigned int*)&flags[0]) return;
+    const uint64_t key = keys[m0];
+    if (m0 > 0 && keys[m0 - 1] == key) return;                          // not the first of its run
     const int R = p.R;
-    const int64_t idx = keys[k];
+    const int64_t idx = (int64_t)key;
     const int64_t i = idx / R;
-    const int r = (int)(idx % R);
+    const int r = (int)(idx - i * R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
     RepState x;
     load_rep(x, p, idx);
     const LogView lv = log_of(p, idx);
     derive_cache(x, lv);
     BatchCounters cnt;
-    for (int64_t m = off[k]; m < off[k + 1]; ++m) {
-        const int64_t o = order[m];
+    for (int m = m0; m < n && keys[m] == key; ++m) {
+        const uint32_t o = order[m];
         if (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
         resolve_rep_draw(x, p, t, gid, r);
     }
     store_rep(x, p, idx);
-    if (cnt.miss) atomicAdd(misses, cnt.miss);
+    if (cnt.miss) atomicAdd(&flags[1], cnt.miss);
 }
 
 // read_log / write_log: the host's [n][R][log_cap] image of groups [g0, g0+n)
@@ -673,6 +700,15 @@ struct raft_engine {
     hipStream_t sub_stream[RAFT_MAX_SUBRANGES];
     hipEvent_t ev_fork, ev_sub_done[RAFT_MAX_SUBRANGES], ev_red_done[2];
     uint64_t launches_issued;   // step launches (all sub-ranges) so far: the partials buffer parity
+    // batch path staging, grow-only: device scratch (keys, sort), device
+    // copies of host batches, pinned host staging, pinned status flags
+    char* bst;
+    size_t bst_bytes;
+    char* bio;
+    size_t bio_bytes;
+    char* hst;
+    size_t hst_bytes;
+    unsigned int* bflags_host;
     int64_t* counters_dev;      // [K][STRIDE] scratch
     int nchunks;                // counter-reduction chunks of REDUCE_CHUNK partials
     unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
@@ -819,6 +855,9 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->ev_fork = nullptr;
     for (int q = 0; q < RAFT_MAX_SUBRANGES; ++q) { e->sub_stream[q] = nullptr; e->ev_sub_done[q] = nullptr; }
     e->ev_red_done[0] = e->ev_red_done[1] = nullptr;
+    e->bst = e->bio = e->hst = nullptr;
+    e->bst_bytes = e->bio_bytes = e->hst_bytes = 0;
+    e->bflags_host = nullptr;
     e->device = device;
     e->t = 0;
     const int64_t G = p->G, R = p->R;
@@ -879,6 +918,12 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->accum = (unsigned long long*)b; b += al(acc_b);
     d.log = (uint2*)b;
     *out = e;
+    err = hipHostMalloc((void**)&e->bflags_host, 64, hipHostMallocDefault);
+    if (err != hipSuccess) {
+        raft_engine_destroy(e);
+        *out = nullptr;
+        return fail(RAFT_ENOMEM, "hipHostMalloc of the batch status flags failed");
+    }
     if (int rc = raft_engine_set_subranges(e, p->subranges)) {
         raft_engine_destroy(e);
         *out = nullptr;
@@ -923,6 +968,10 @@ int raft_engine_destroy(raft_engine* e) {
     }
     for (hipEvent_t x : {e->ev_fork, e->ev_red_done[0], e->ev_red_done[1]})
         if (x) (void)hipEventDestroy(x);
+    if (e->bst) (void)hipFree(e->bst);
+    if (e->bio) (void)hipFree(e->bio);
+    if (e->hst) (void)hipHostFree(e->hst);
+    if (e->bflags_host) (void)hipHostFree(e->bflags_host);
     (void)hipFree(e->base);
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1239,57 +1288,110 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
     return RAFT_OK;
 }
 
-static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
-                     size_t req_sz, void* resp, size_t resp_sz, int64_t n) {
-    if (!e) return fail(RAFT_EINVAL, "null engine");
-    if (n < 0) return fail(RAFT_EINVAL, "negative batch");
-    if (n == 0) return RAFT_OK;
-    if (!group || !dst || !req || (resp_sz && !resp)) return fail(RAFT_EINVAL, "null buffer");
+// Grow-only engine staging of the batch path (no allocation, and so no
+// device-wide hipFree synchronisation, once a batch size has been seen).
+static int grow_dev(raft_engine* e, char** buf, size_t* have, size_t need) {
+    if (need <= *have) return RAFT_OK;
+    if (*buf) HIP_TRY(hipFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    need = std::max(need, (size_t)1 << 20) * 5 / 4;
+    HIP_TRY(hipMalloc((void**)buf, need));
+    *have = need;
+    return RAFT_OK;
+}
+static int grow_host(raft_engine* e, char** buf, size_t* have, size_t need) {
+    if (need <= *have) return RAFT_OK;
+    if (*buf) HIP_TRY(hipHostFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    need = std::max(need, (size_t)1 << 20) * 5 / 4;
+    HIP_TRY(hipHostMalloc((void**)buf, need, hipHostMallocDefault));
+    *have = need;
+    return RAFT_OK;
+}
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// The batch on device buffers: keys, a stable radix sort over the key bits,
+// the handlers; one synchronisation at the end for the status flags.
+static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                         void* resp, int64_t n64) {
+    const int n = (int)n64;
     const int R = e->p.R;
-    std::vector<int64_t> key(n);
-    for (int64_t m = 0; m < n; ++m) {
-        if (group[m] < 0 || group[m] >= e->p.G) return fail(RAFT_ERANGE, "group outside the engine");
-        if (dst[m] < 0 || dst[m] >= R) return fail(RAFT_EINVAL, "replica index outside 0..R-1");
-        key[m] = group[m] * R + dst[m];
-    }
-    std::vector<int64_t> order(n);
-    for (int64_t m = 0; m < n; ++m) order[m] = m;
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return key[a] < key[b]; });
-    std::vector<int64_t> keys, off;
-    for (int64_t m = 0; m < n; ++m) {
-        if (m == 0 || key[order[m]] != key[order[m - 1]]) { keys.push_back(key[order[m]]); off.push_back(m); }
-    }
-    off.push_back(n);
-    const int nk = (int)keys.size();
-    HIP_TRY(hipSetDevice(e->device));
+    int bits = 1;
+    while (bits < 64 && ((uint64_t)e->p.G * (uint64_t)R - 1) >> bits) ++bits;
+    size_t sort_tmp = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                               (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, bits, e->stream));
+    const size_t b_keys = al256((size_t)n * 8), b_ord = al256((size_t)n * 4);
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, 2 * b_keys + 2 * b_ord + al256(sort_tmp) + 256)) return rc;
+    char* b = e->bst;
+    uint64_t* k_in = (uint64_t*)b; b += b_keys;
+    uint64_t* k_out = (uint64_t*)b; b += b_keys;
+    uint32_t* o_in = (uint32_t*)b; b += b_ord;
+    uint32_t* o_out = (uint32_t*)b; b += b_ord;
+    unsigned int* flags = (unsigned int*)b; b += 256;
+    void* tmp = b;
+    HIP_TRY(hipMemsetAsync(flags, 0, 8, e->stream));
+    const unsigned grid = (unsigned)((n + BLOCK - 1) / BLOCK);
+    batch_keys_kernel<<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, k_in, o_in, flags);
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, sort_tmp, k_in, k_out, o_in, o_out, n, 0, bits, e->stream));
+    auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true> : batch_kernel<false>;
+    kern<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, kind, n, k_out, o_out, req, resp, flags);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     e->cache_valid = false;
-    const size_t b_keys = nk * 8, b_off = (nk + 1) * 8, b_ord = n * 8, b_req = n * req_sz, b_resp = n * resp_sz;
-    char* buf = nullptr;
-    HIP_TRY(hipMalloc(&buf, b_keys + b_off + b_ord + b_req + b_resp + 64));
-    char* pk = buf; char* po = pk + b_keys; char* pd = po + b_off; char* pq = pd + b_ord; char* ps = pq + b_req;
-    unsigned int* pm = (unsigned int*)(ps + ((b_resp + 7) & ~(size_t)7));      // window-miss count
-    unsigned int misses = 0;
-    hipError_t err = hipMemsetAsync(pm, 0, 4, e->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(pk, keys.data(), b_keys, hipMemcpyHostToDevice, e->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(po, off.data(), b_off, hipMemcpyHostToDevice, e->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(pd, order.data(), b_ord, hipMemcpyHostToDevice, e->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(pq, req, b_req, hipMemcpyHostToDevice, e->stream);
-    if (err == hipSuccess) {
-        auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true> : batch_kernel<false>;
-        kern<<<(nk + BLOCK - 1) / BLOCK, BLOCK, 0, e->stream>>>(
-            e->dp, (uint32_t)e->t, kind, nk, (const int64_t*)pk, (const int64_t*)po, (const int64_t*)pd, pq,
-            resp_sz ? (void*)ps : nullptr, pm);
-        err = hipGetLastError();
-    }
-    if (err == hipSuccess && resp_sz) err = hipMemcpyAsync(resp, ps, b_resp, hipMemcpyDeviceToHost, e->stream);
-    if (err == hipSuccess) err = hipMemcpyAsync(&misses, pm, 4, hipMemcpyDeviceToHost, e->stream);
-    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-    (void)hipFree(buf);
-    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
-    if (misses)
-        return fail(RAFT_EWINDOW, std::to_string(misses) + " log accesses below the retained log_window: "
+    if (e->bflags_host[0]) return fail(RAFT_ERANGE, "a message's group or replica index is outside the engine; "
+                                                    "nothing was applied");
+    if (e->bflags_host[1])
+        return fail(RAFT_EWINDOW, std::to_string(e->bflags_host[1]) + " log accesses below the retained log_window: "
                                   "the batch's results are not the reference's");
     return RAFT_OK;
+}
+
+static int check_batch_args(raft_engine* e, int64_t n, const void* group, const void* dst, const void* req,
+                            size_t resp_sz, const void* resp) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (n < 0) return fail(RAFT_EINVAL, "negative batch");
+    if (n > 0x7FFFFFFF) return fail(RAFT_EINVAL, "batch larger than 2^31 - 1 messages");
+    if (n > 0 && (!group || !dst || !req || (resp_sz && !resp))) return fail(RAFT_EINVAL, "null buffer");
+    return RAFT_OK;
+}
+
+// Host buffers: copied into engine-owned pinned staging (one memcpy per
+// array), moved to device staging with one DMA, run on the device, and the
+// responses copied back the same way.
+static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                     size_t req_sz, void* resp, size_t resp_sz, int64_t n) {
+    if (int rc = check_batch_args(e, n, group, dst, req, resp_sz, resp)) return rc;
+    if (n == 0) return RAFT_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t b_g = al256((size_t)n * 8), b_d = al256((size_t)n * 4), b_q = al256((size_t)n * req_sz);
+    const size_t b_s = al256((size_t)n * resp_sz), in_b = b_g + b_d + b_q;
+    if (int rc = grow_host(e, &e->hst, &e->hst_bytes, in_b + b_s)) return rc;
+    if (int rc = grow_dev(e, &e->bio, &e->bio_bytes, in_b + b_s)) return rc;
+    std::memcpy(e->hst, group, (size_t)n * 8);
+    std::memcpy(e->hst + b_g, dst, (size_t)n * 4);
+    std::memcpy(e->hst + b_g + b_d, req, (size_t)n * req_sz);
+    HIP_TRY(hipMemcpyAsync(e->bio, e->hst, in_b, hipMemcpyHostToDevice, e->stream));
+    const int rc = run_batch_dev(e, kind, (const int64_t*)e->bio, (const int32_t*)(e->bio + b_g), e->bio + b_g + b_d,
+                                 resp_sz ? e->bio + in_b : nullptr, n);
+    if (rc != RAFT_OK && rc != RAFT_EWINDOW) return rc;
+    if (resp_sz) {
+        HIP_TRY(hipMemcpyAsync(e->hst + in_b, e->bio + in_b, (size_t)n * resp_sz, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        std::memcpy(resp, e->hst + in_b, (size_t)n * resp_sz);
+    }
+    return rc;
+}
+
+static int run_batch_on_device(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                               size_t resp_sz, void* resp, int64_t n) {
+    if (int rc = check_batch_args(e, n, group, dst, req, resp_sz, resp)) return rc;
+    if (n == 0) return RAFT_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    return run_batch_dev(e, kind, group, dst, req, resp, n);
 }
 
 int raft_vote_batch(raft_engine* e, const int64_t* group, const int32_t* dst, const raft_vote_req* req,
@@ -1305,6 +1407,21 @@ int raft_append_batch(raft_engine* e, const int64_t* group, const int32_t* dst, 
 int raft_append_command_batch(raft_engine* e, const int64_t* group, const int32_t* replica, const uint32_t* cmd,
                               int64_t n) {
     return run_batch(e, BATCH_COMMAND, group, replica, cmd, sizeof(uint32_t), nullptr, 0, n);
+}
+
+int raft_vote_batch_dev(raft_engine* e, const int64_t* group, const int32_t* dst, const raft_vote_req* req,
+                        raft_vote_resp* resp, int64_t n) {
+    return run_batch_on_device(e, BATCH_VOTE, group, dst, req, sizeof(raft_vote_resp), resp, n);
+}
+
+int raft_append_batch_dev(raft_engine* e, const int64_t* group, const int32_t* dst, const raft_append_req* req,
+                          raft_append_resp* resp, int64_t n) {
+    return run_batch_on_device(e, BATCH_APPEND, group, dst, req, sizeof(raft_append_resp), resp, n);
+}
+
+int raft_append_command_batch_dev(raft_engine* e, const int64_t* group, const int32_t* replica, const uint32_t* cmd,
+                                  int64_t n) {
+    return run_batch_on_device(e, BATCH_COMMAND, group, replica, cmd, 0, nullptr, n);
 }
 
 }  // extern "C"
