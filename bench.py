@@ -261,6 +261,10 @@ def parse_args(argv=None):
     ap.add_argument("--reduce-every", type=int, default=512,
                     help="steps per counter all-reduce (rounded to whole launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--handler-batch", type=int, default=1_000_000,
+                    help="messages per single-handler batch of the handler_batch leg (0 = skip the leg)")
+    ap.add_argument("--handler-reps", type=int, default=20)
+    ap.add_argument("--handler-sample", type=int, default=128, help="groups checked against the oracle")
     ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target seconds of the SoA leg on every core")
@@ -326,6 +330,114 @@ def cpu_baseline(args, kw, log_cap, total_steps):
                        "oracle/raft_oracle.c (scalar C restatement of RaftServer.kt/Commons.kt), pthreads; ")
                       + best["sample"],
             "legs": legs, "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+
+
+def handler_requests(rng, n, G, R, max_term):
+    """n random single-handler messages over the engine's G x R replicas:
+    (group, dst, vote requests [n, 4], append requests [n, 8] as int32 bit
+    patterns).  Vote fields are drawn around the run's terms; half the appends
+    carry prevLogIndex -1 (the consistency check passes and, with an entry,
+    Log.add(0) overwrites and truncates: Q2), half a random prevLogIndex below
+    64 with a random prevLogTerm (mostly rejected)."""
+    group = rng.integers(0, G, n, dtype=np.int64)
+    dst = rng.integers(0, R, n).astype(np.int32)
+    vote = np.stack([rng.integers(0, 2 * max_term + 2, n), rng.integers(1, R + 1, n), rng.integers(0, 4000, n),
+                     rng.integers(0, max_term + 1, n)], axis=1).astype(np.int32)
+    prev = np.where(rng.random(n) < 0.5, -1, rng.integers(0, 64, n))
+    app = np.stack([rng.integers(0, 2 * max_term + 2, n), rng.integers(1, R + 1, n), prev,
+                    rng.integers(0, max_term + 1, n), rng.integers(0, 2, n), rng.integers(0, max_term + 1, n),
+                    rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.int64), rng.integers(0, 4000, n)],
+                   axis=1).astype(np.int64).astype(np.uint32).view(np.int32)
+    return group, dst, vote, app
+
+
+def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
+    """The drop-in service path (RaftServer.vote() / append(), RaftServer.kt:228-287):
+    raft_vote_batch_dev / raft_append_batch_dev on n random messages already
+    in HBM (key, stable radix sort, one lane per replica run), and the same
+    through the host entry points (pinned staging and PCIe both ways).  The
+    first device batch of each kind is checked against the oracle's handlers
+    on a sample of groups: each sampled group's state and log are copied into
+    its own oracle, which applies the batch's messages to that group in batch
+    order; responses, state and logs must be equal."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n = args.handler_batch
+    st = eng.read_state()
+    max_term = int(st[:, [r * abi.NUM_FIELDS + abi.F_INDEX["term"] for r in range(R)]].max())
+    rng = np.random.default_rng(12345)
+    group, dst, vote, app = handler_requests(rng, n, G, R, max_term)
+    sample = np.sort(rng.choice(G, size=min(G, args.handler_sample), replace=False))
+    t_step = eng.step_index
+    out = {"messages_per_batch": n, "groups": G, "replicas": R}
+    for kind, req, resp_w in (("vote", vote, 2), ("append", app, 3)):
+        pre = {int(g): (eng.read_state(int(g), 1), *eng.read_log(int(g), 1)) for g in sample}
+        d_group = torch.from_numpy(group).to(dev)
+        d_dst = torch.from_numpy(dst).to(dev)
+        d_req = torch.from_numpy(np.ascontiguousarray(req)).to(dev)
+        d_resp = torch.zeros((n, resp_w), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        fn = eng.vote_batch_dev if kind == "vote" else eng.append_batch_dev
+        ptrs = (d_group.data_ptr(), d_dst.data_ptr(), d_req.data_ptr(), d_resp.data_ptr(), n)
+        fn(*ptrs)                                                       # the parity batch
+        resp = d_resp.cpu().numpy()
+        # oracle replay on the sample
+        sel = np.isin(group, sample)
+        bad = 0
+        for g in sample:
+            s0, t0, c0 = pre[int(g)]
+            o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(params_kw, G=1, g0=int(g))))
+            o.write_state(s0)
+            o.write_log(t0, c0)
+            o.step_index = t_step
+            for m in np.nonzero(sel & (group == g))[0]:
+                q = req[m]
+                if kind == "vote":
+                    got = tuple(int(x) for x in resp[m])
+                    want = o.vote(0, int(dst[m]), *(int(x) for x in q))
+                    want = (int(want[0]), int(want[1]))
+                else:
+                    qq = q.view(np.uint32).astype(np.int64)
+                    t_, s_, st_ = o.append(0, int(dst[m]), int(q[0]), int(q[1]), int(q[2]), int(q[3]),
+                                           (int(q[5]), int(qq[6])) if q[4] else None, int(q[7]))
+                    got, want = tuple(int(x) for x in resp[m]), (int(t_), int(s_), int(st_))
+                bad += got != want
+            es, (et, ec) = eng.read_state(int(g), 1), eng.read_log(int(g), 1)
+            os_, (ot, oc) = o.read_state(), o.read_log()
+            bad += not np.array_equal(es, os_)
+            phys = es[0, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(R)]]
+            for r in range(R):
+                k = int(phys[r])
+                bad += not (np.array_equal(et[0, r, :k], ot[0, r, :k]) and np.array_equal(ec[0, r, :k], oc[0, r, :k]))
+            o.close()
+        # timed: device-resident batches (each call returns after its batch finished)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.handler_reps):
+            fn(*ptrs)
+        dt_dev = time.perf_counter() - t0
+        # timed: host buffers (pinned staging + PCIe both ways)
+        hfn = eng.vote_batch if kind == "vote" else eng.append_batch
+        hreq = req
+        t0 = time.perf_counter()
+        reps_h = max(1, args.handler_reps // 4)
+        for _ in range(reps_h):
+            hfn(group, dst, hreq)
+        dt_host = time.perf_counter() - t0
+        out[kind] = {"messages_per_s_device": n * args.handler_reps / dt_dev,
+                     "ms_per_batch_device": dt_dev * 1e3 / args.handler_reps,
+                     "messages_per_s_host_buffers": n * reps_h / dt_host,
+                     "ms_per_batch_host_buffers": dt_host * 1e3 / reps_h,
+                     "parity_sample_groups": int(sample.size), "parity_sample_messages": int(sel.sum()),
+                     "parity_mismatches": int(bad)}
+    out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a key kernel, a stable hipcub radix sort "
+                   "over the key bits, the handler kernel (one lane per replica run, messages in batch order) and "
+                   "one status synchronisation; _host_buffers: the same through the host entry points (engine-owned "
+                   "pinned staging, PCIe both ways). The engine holds the bench run's final state; the messages are "
+                   "random (bench.handler_requests). Parity: the first batch of each kind against the oracle's "
+                   "handlers on the sampled groups")
+    return out
 
 
 def plan_only(args, world, rank):
@@ -638,6 +750,9 @@ def main(argv=None, result=None):
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
+    if args.handler_batch > 0 and world == 1 and not coll:
+        out["handler_batch"] = handler_batch_leg(eng, args, dict(kw, mode=mode, ae_max_entries=args.ae_max_entries),
+                                                 log_cap, dev, G_local, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, dict(kw, mode=mode, ae_max_entries=args.ae_max_entries), log_cap,
                                            args.warmup + args.steps)

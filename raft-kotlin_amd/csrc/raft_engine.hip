@@ -700,6 +700,7 @@ struct raft_engine {
     hipStream_t sub_stream[RAFT_MAX_SUBRANGES];
     hipEvent_t ev_fork, ev_sub_done[RAFT_MAX_SUBRANGES], ev_red_done[2];
     uint64_t launches_issued;   // step launches (all sub-ranges) so far: the partials buffer parity
+    bool fork_needed;           // the engine stream holds work the sub-range streams have not waited for
     // batch path staging, grow-only: device scratch (keys, sort), device
     // copies of host batches, pinned host staging, pinned status flags
     char* bst;
@@ -852,6 +853,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->timed_launches = 0;
     e->nsub = 1;
     e->launches_issued = 0;
+    e->fork_needed = true;
     e->ev_fork = nullptr;
     for (int q = 0; q < RAFT_MAX_SUBRANGES; ++q) { e->sub_stream[q] = nullptr; e->ev_sub_done[q] = nullptr; }
     e->ev_red_done[0] = e->ev_red_done[1] = nullptr;
@@ -996,6 +998,7 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
     if (!e->cache_valid && n_steps > 0) {
         rebuild_cache_kernel<<<(unsigned)((e->dp.GR + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp);
         e->cache_valid = true;
+        e->fork_needed = true;
     }
     // One sub-range: every launch and its counter reduction on the engine
     // stream.  nsub > 1: launch k of sub-range q runs on sub_stream[q] and
@@ -1005,11 +1008,18 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
     // waits for.  A sub-range thus runs up to a launch ahead of another, and
     // its launches follow each other without waiting for the other ranges'
     // tails.  Work enqueued on the engine stream after this call sees every
-    // launch finished (the last reductions wait for all of them).
+    // launch finished (the last reductions wait for all of them).  The
+    // sub-range streams wait for the engine stream only when an engine call
+    // other than a step enqueued work there since (fork_needed): waiting for
+    // the previous call's reductions would re-join the ranges at every call,
+    // and bench.py calls once per launch.  Callers must not change the
+    // engine's device state on the engine stream themselves (it is engine
+    // memory; the API calls that do, set fork_needed).
     const bool split = e->nsub > 1;
-    if (split && n_steps > 0) {
+    if (split && n_steps > 0 && e->fork_needed) {
         HIP_TRY(hipEventRecord(e->ev_fork, e->stream));
         for (int q = 0; q < e->nsub; ++q) HIP_TRY(hipStreamWaitEvent(e->sub_stream[q], e->ev_fork, 0));
+        e->fork_needed = false;
     }
     for (int32_t done = 0; done < n_steps;) {
         const int k = std::min<int32_t>(e->K, n_steps - done);
@@ -1159,6 +1169,7 @@ int raft_engine_read_state(raft_engine* e, int64_t g0, int64_t n, int32_t* out) 
     if (n == 0) return RAFT_OK;
     if (!out) return fail(RAFT_EINVAL, "null buffer");
     HIP_TRY(hipSetDevice(e->device));
+    e->fork_needed = true;
     const size_t bytes = (size_t)n * raft_group_words(e->p.R) * 4;
     int32_t* buf = nullptr;
     HIP_TRY(hipMalloc(&buf, bytes));
@@ -1182,6 +1193,7 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
                 return fail(RAFT_EINVAL, "state violates 0 <= lastIndex <= physLen <= log_cap");
         }
     HIP_TRY(hipSetDevice(e->device));
+    e->fork_needed = true;
     const size_t bytes = (size_t)n * W * 4;
     int32_t* buf = nullptr;
     HIP_TRY(hipMalloc(&buf, bytes));
@@ -1198,6 +1210,7 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
 
 // the [n][R][log_cap] host image of groups [g0, g0+n) through a device buffer
 static int log_image(raft_engine* e, int64_t g0, int64_t n, std::vector<uint2>& tmp, bool to_ring) {
+    e->fork_needed = true;
     const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
     uint2* buf = nullptr;
     HIP_TRY(hipMalloc(&buf, cnt * 8));
@@ -1250,6 +1263,7 @@ int raft_engine_digest_range(raft_engine* e, int64_t g0, int64_t n, uint64_t* ou
     *out = 0;
     if (n == 0) return RAFT_OK;
     HIP_TRY(hipSetDevice(e->device));
+    e->fork_needed = true;
     unsigned long long* d = nullptr;
     HIP_TRY(hipMalloc(&d, 8));
     hipError_t err = hipMemsetAsync(d, 0, 8, e->stream);
@@ -1267,6 +1281,7 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
     if (int rc = check_range(e, g0, n)) return rc;
     if (!mismatched) return fail(RAFT_EINVAL, "null argument");
     HIP_TRY(hipSetDevice(e->device));
+    e->fork_needed = true;
     *mismatched = 0;
     if (n == 0) return RAFT_OK;
     void* d = nullptr;
@@ -1316,6 +1331,7 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // the handlers; one synchronisation at the end for the status flags.
 static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
                          void* resp, int64_t n64) {
+    e->fork_needed = true;
     const int n = (int)n64;
     const int R = e->p.R;
     int bits = 1;

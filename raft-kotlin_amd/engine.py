@@ -193,7 +193,11 @@ class RaftEngine:
     def append_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
         """req: [n, 8] int32 (term, leaderId, prevLogIndex, prevLogTerm, hasEntry,
         entryTerm, entryCmd(u32 bits), leaderCommit) -> [n, 3] (term, success, status)."""
-        q = np.ascontiguousarray(req).astype(np.int64).astype(np.uint32).view(np.int32).reshape(-1, 8)
+        req = np.asarray(req)
+        if req.dtype == np.int32 or req.dtype == np.uint32:       # already the struct's 32-bit words
+            q = np.ascontiguousarray(req).view(np.int32).reshape(-1, 8)
+        else:
+            q = np.ascontiguousarray(req).astype(np.int64).astype(np.uint32).view(np.int32).reshape(-1, 8)
         g, d = self._batch_index(group, dst, q.shape[0], "append_batch")
         out = np.zeros((q.shape[0], 3), dtype=np.int32)
         self._check(self._lib.raft_append_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
@@ -209,6 +213,23 @@ class RaftEngine:
         self._check(self._lib.raft_append_command_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(r, C.c_int32),
                                                         abi.ptr(c, C.c_uint32), c.shape[0]),
                     "raft_append_command_batch")
+
+
+    # -- the same batches on device buffers (HBM-resident inputs) ------------
+    def vote_batch_dev(self, group_ptr: int, dst_ptr: int, req_ptr: int, resp_ptr: int, n: int):
+        """raft_vote_batch_dev: DEVICE pointers to n int64 groups, int32
+        replicas, raft_vote_req and raft_vote_resp (e.g. torch tensors'
+        data_ptr() on this engine's GPU)."""
+        self._check(self._lib.raft_vote_batch_dev(self._h, group_ptr, dst_ptr, req_ptr, resp_ptr, int(n)),
+                    "raft_vote_batch_dev")
+
+    def append_batch_dev(self, group_ptr: int, dst_ptr: int, req_ptr: int, resp_ptr: int, n: int):
+        self._check(self._lib.raft_append_batch_dev(self._h, group_ptr, dst_ptr, req_ptr, resp_ptr, int(n)),
+                    "raft_append_batch_dev")
+
+    def append_command_batch_dev(self, group_ptr: int, replica_ptr: int, cmd_ptr: int, n: int):
+        self._check(self._lib.raft_append_command_batch_dev(self._h, group_ptr, replica_ptr, cmd_ptr, int(n)),
+                    "raft_append_command_batch_dev")
 
 
 def philox4x32_10(ctr, key):

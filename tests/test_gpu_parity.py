@@ -425,10 +425,15 @@ def random_states(rng, n, R, cap):
     return w, logs_t, logs_c
 
 
-@pytest.mark.parametrize("mode", [abi.MODE_REFERENCE, abi.MODE_TEXTBOOK])
-def test_handler_batches_vs_oracle(mode):
+@pytest.mark.parametrize("mode,G,n", [(abi.MODE_REFERENCE, 64, 3000), (abi.MODE_TEXTBOOK, 64, 3000),
+                                      (abi.MODE_REFERENCE, 4000, 100_000)])
+def test_handler_batches_vs_oracle(mode, G, n):
+    """The single-handler batches (RaftServer.vote() / append() /
+    appendCommand(), RaftServer.kt:228-287, :100-107) against the oracle's
+    handlers message by message: at n = 3000 on 64 groups (long runs of
+    messages per replica) and at n = 10^5 on 4000 groups."""
     rng = np.random.default_rng(7)
-    R, G, cap, n = 5, 64, 8, 3000
+    R, cap = 5, 8
     w, lt, lc = random_states(rng, G, R, cap)
     e, o = pair(R=R, G=G, log_cap=cap, seed=3, mode=mode)
     for x in (e, o):
@@ -458,6 +463,53 @@ def test_handler_batches_vs_oracle(mode):
     se = e.read_state()
     assert_same_state(se, o.read_state(), R, "handlers")
     assert_same_logs(se, e.read_log(), o.read_log(), R, "handlers")
+
+
+def test_device_batches_match_host_batches():
+    """raft_*_batch_dev on HBM-resident messages (torch tensors) leave the
+    same responses, state and logs as the host entry points on an identical
+    engine; a message outside the engine fails the whole batch with
+    RAFT_ERANGE before anything is applied."""
+    import torch
+    rng = np.random.default_rng(11)
+    R, G, cap, n = 5, 500, 8, 20_000
+    w, lt, lc = random_states(rng, G, R, cap)
+    a, b = (RaftEngine(abi.make_params(R=R, G=G, log_cap=cap, seed=3)) for _ in range(2))
+    for x in (a, b):
+        x.write_state(w)
+        x.write_log(lt, lc)
+    grp = rng.integers(0, G, size=n)
+    dst = rng.integers(0, R, size=n).astype(np.int32)
+    vq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(0, cap + 1, n),
+                   rng.integers(0, 4, n)], axis=1).astype(np.int32)
+    aq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(-1, cap, n),
+                   rng.integers(-1, 4, n), rng.integers(0, 2, n), rng.integers(0, 6, n),
+                   rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)], axis=1).astype(np.int64)
+    cmd = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    dev = torch.device("cuda", 0)
+    tg, td = torch.from_numpy(grp.astype(np.int64)).to(dev), torch.from_numpy(dst).to(dev)
+    ve = a.vote_batch(grp, dst, vq)
+    tv, tvr = torch.from_numpy(vq).to(dev), torch.zeros((n, 2), dtype=torch.int32, device=dev)
+    b.vote_batch_dev(tg.data_ptr(), td.data_ptr(), tv.data_ptr(), tvr.data_ptr(), n)
+    assert np.array_equal(ve, tvr.cpu().numpy())
+    ae = a.append_batch(grp, dst, aq)
+    ta = torch.from_numpy(aq.astype(np.uint32).view(np.int32)).to(dev)
+    tar = torch.zeros((n, 3), dtype=torch.int32, device=dev)
+    b.append_batch_dev(tg.data_ptr(), td.data_ptr(), ta.data_ptr(), tar.data_ptr(), n)
+    assert np.array_equal(ae, tar.cpu().numpy())
+    a.append_command_batch(grp, dst, cmd)
+    tc = torch.from_numpy(cmd.view(np.int32)).to(dev)
+    b.append_command_batch_dev(tg.data_ptr(), td.data_ptr(), tc.data_ptr(), n)
+    sa = a.read_state()
+    assert np.array_equal(sa, b.read_state())
+    assert_same_logs(sa, a.read_log(), b.read_log(), R, "device vs host batches")
+    assert a.digest() == b.digest()
+    # an out-of-range message: nothing applied
+    bad_g = grp.copy()
+    bad_g[n // 2] = G
+    with pytest.raises(RuntimeError):
+        a.vote_batch(bad_g, dst, vq)
+    assert np.array_equal(a.read_state(), sa) and a.digest() == b.digest()
 
 
 def test_service_wire_path_matches_batches():
