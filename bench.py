@@ -527,6 +527,7 @@ def main(argv=None, result=None):
     params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=args.subranges,
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
+    nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
     gcounters = torch.zeros_like(counters) if coll else counters
@@ -667,8 +668,10 @@ def main(argv=None, result=None):
                      "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
     if args.plan_file and rank == 0:
-        seq = [["warmup", x] for x in launch_plan(args.warmup, L)] + [["timed", x] for x in timed_plan]
-        seq += [["streaming", 1]] * args.stream_steps
+        # [leg, steps, dispatches]: a launch of the warmup / timed legs is one
+        # step-kernel dispatch per sub-range; the streaming leg runs one range
+        seq = [["warmup", x, nsub] for x in launch_plan(args.warmup, L)] + [["timed", x, nsub] for x in timed_plan]
+        seq += [["streaming", 1, 1]] * args.stream_steps
         json.dump({"key": pmc_key, "stream_steps": args.stream_steps, "R": R, "launches": seq},
                   open(args.plan_file, "w"))
 
@@ -715,7 +718,7 @@ def main(argv=None, result=None):
             "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
             "log_window": window, "hbm_bytes_engine": eng.device_bytes,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
-            "subranges": eng.subranges,
+            "subranges": nsub,
             "step_waves_per_rank": -(-G_local // (64 // R)),
             "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window) < abi.MAX_STEPS_PER_LAUNCH),
             "counter_allreduce_every": chunk if coll else None,

@@ -36,15 +36,37 @@ def dispatches(d):
     return {c: [v for _, v in sorted(x.items())] for c, x in acc.items()}
 
 
-def traced_ms(d):
-    """[duration ms per step_kernel dispatch, in dispatch order] from the
-    --kernel-trace run of the same command (empty if absent)."""
+def traced(d):
+    """[(start ns, end ns) per step_kernel dispatch, in dispatch order] from
+    the --kernel-trace run of the same command (empty if absent)."""
     rows = []
     for f in glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if "step_kernel" in row["Kernel_Name"]:
-                rows.append((int(row["Dispatch_Id"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
+                rows.append((int(row["Dispatch_Id"]), (int(row["Start_Timestamp"]), int(row["End_Timestamp"]))))
     return [v for _, v in sorted(rows)]
+
+
+def union_ms(iv):
+    """Time covered by the intervals (ns pairs), in ms: bench.py's step-kernel
+    time when launch sub-ranges overlap."""
+    acc, lo, hi = 0, None, None
+    for a, b in sorted(iv):
+        if hi is None or a > hi:
+            if hi is not None:
+                acc += hi - lo
+            lo, hi = a, b
+        else:
+            hi = max(hi, b)
+    return (acc + (hi - lo if hi is not None else 0)) / 1e6
+
+
+def expand(seq):
+    """Plan launches [leg, steps(, dispatches)] -> (launch index per dispatch)."""
+    out = []
+    for i, x in enumerate(seq):
+        out += [i] * (x[2] if len(x) > 2 else 1)
+    return out
 
 
 def mean(xs):
@@ -59,19 +81,25 @@ def main(d):
     cw = sorted(dispatches(f"{d}/calib_WRITE_SIZE").get("WRITE_SIZE", []))
     ff = state / (cf[len(cf) // 2] * 1024.0)
     wf = state / (cw[len(cw) // 2] * 1024.0)
+    owner = expand(seq)
     per = {}
     for p in sorted(glob.glob(f"{d}/pmc*")):
         for c, vals in dispatches(p).items():
-            if len(vals) != len(seq):
-                raise SystemExit(f"{p}: {len(vals)} step_kernel dispatches, plan has {len(seq)}")
-            per[c] = vals
-    tr = traced_ms(d)
+            if len(vals) != len(owner):
+                raise SystemExit(f"{p}: {len(vals)} step_kernel dispatches, plan has {len(owner)}")
+            acc = [0.0] * len(seq)                     # a launch = the sum of its sub-range dispatches
+            for k, v in zip(owner, vals):
+                acc[k] += v
+            per[c] = acc
+    trd = traced(d)
     rows = []
     for leg in ("timed", "streaming"):
-        ix = [i for i, (lg, _) in enumerate(seq) if lg == leg]
+        ix = [i for i, x in enumerate(seq) if x[0] == leg]
         if not ix:
             continue
         steps = {seq[i][1] for i in ix}
+        trace_ms = (union_ms([iv for k, iv in zip(owner, trd) if k in set(ix)]) / len(ix)
+                    if len(trd) == len(owner) else None)
         if len(steps) != 1:
             continue                                   # mixed launch lengths: no per-launch row
         m = {c: mean([v[i] for i in ix]) for c, v in per.items()}
@@ -93,9 +121,13 @@ def main(d):
             # every counter of every pass, per launch (the stall split:
             # SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~= SQ_WAVE_CYCLES)
             "pmc_raw": {c: v for c, v in sorted(m.items())},
-            "trace_avg_ms": mean([tr[i] for i in ix]) if len(tr) == len(seq) else None,
-            "effective_clock_ghz": (m["GRBM_GUI_ACTIVE"] / 8 / (mean([tr[i] for i in ix]) / 1e3) / 1e9
-                                    if len(tr) == len(seq) and m.get("GRBM_GUI_ACTIVE") else None),
+            "trace_avg_ms": trace_ms,
+            "dispatches_per_launch": seq[ix[0]][2] if len(seq[ix[0]]) > 2 else 1,
+            # (rocprofv3 --pmc serialises dispatches, so GRBM_GUI_ACTIVE of
+            # overlapping sub-range dispatches does not time one launch)
+            "effective_clock_ghz": (m["GRBM_GUI_ACTIVE"] / 8 / (trace_ms / 1e3) / 1e9
+                                    if trace_ms and m.get("GRBM_GUI_ACTIVE") and
+                                    (len(seq[ix[0]]) < 3 or seq[ix[0]][2] == 1) else None),
             "source": f"rocprofv3 --pmc, separate passes (scripts/pmc_bench.sh, {os.path.basename(d)})",
         })
         rows.append(row)

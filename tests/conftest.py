@@ -7,6 +7,16 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
 
 
+# torch ships its own HIP runtime (same soname as /opt/rocm's): import it
+# before the engine library is loaded, so every test process uses one HIP
+# runtime whatever order its tests run in (bench.py imports torch first too).
+# Importing torch does not initialise a GPU.
+try:
+    import torch  # noqa: F401,E402
+except ImportError:
+    pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP engine on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
