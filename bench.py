@@ -524,7 +524,12 @@ def main(argv=None, result=None):
     spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window)
     L = launch_length(args.steps, spl)                      # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
-    params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=args.subranges,
+    # launch sub-ranges: the engine's automatic choice overlaps one range's
+    # last waves with another's next launch; a timed region of ONE launch has
+    # no next launch to overlap, and there one full-grid dispatch is faster
+    # (DESIGN.md §6), so --subranges 0 resolves to 1 for it
+    subranges = args.subranges or (1 if args.steps <= L else 0)
+    params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=subranges,
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs

@@ -18,7 +18,7 @@ out = {"fetch_factor": ff, "write_factor": wf, "variants": {}}
 for plan in sorted(glob.glob(f"{d}/plan_*.json")):
     v = os.path.basename(plan)[5:-5]
     seq = json.load(open(plan))["launches"]
-    ix = [i for i, (leg, _) in enumerate(seq) if leg == "timed"]
+    ix = [i for i, x in enumerate(seq) if x[0] == "timed"]
     row = {"launch_steps": seq[ix[0]][1], "launches": len(ix)}
     for p in sorted(glob.glob(f"{d}/{v}_p*")):
         for c, vals in dispatches(p).items():

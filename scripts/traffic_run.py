@@ -24,12 +24,12 @@ G = int(os.environ.get("TRAFFIC_GROUPS", "1000000"))
 def main(mode):
     if mode == "calib":
         p = abi.make_params(R=5, G=G, seed=3, log_cap=4, election_min_ms=1 << 30, election_max_ms=1 << 30,
-                            steps_per_launch=1)
+                            steps_per_launch=1, subranges=1)      # one dispatch moves the whole state
         e = RaftEngine(p)
         e.step(20, counters=False)
     else:
         kw = dict(abi.CONFIGS[3], G=G)
-        e = RaftEngine(abi.make_params(log_cap=640, steps_per_launch=64, **kw))
+        e = RaftEngine(abi.make_params(log_cap=640, steps_per_launch=64, subranges=1, **kw))
         e.step(128, counters=False)        # warmup (2 launches)
         e.step(256, counters=False)        # 4 launches at K=64
         e.set_steps_per_launch(512)
