@@ -79,11 +79,16 @@ class RaftEngine:
 
     @property
     def subranges(self) -> int:
-        """Launch sub-ranges in use (raft_params.subranges; streams per launch)."""
+        """Launch sub-ranges in use (raft_params.subranges; streams per launch).
+        An older experimental build (RAFT_ENGINE_LIB) without them: 1."""
+        if getattr(self._lib.raft_engine_subranges, "__name__", "") == "stub":
+            return 1
         return int(self._lib.raft_engine_subranges(self._h))
 
     def set_subranges(self, n: int):
         """Split the step launches over n sub-range streams (0 = automatic)."""
+        if getattr(self._lib.raft_engine_set_subranges, "__name__", "") == "stub":
+            return                                   # an older experimental build: one range
         self._check(self._lib.raft_engine_set_subranges(self._h, int(n)), "set_subranges")
 
     @property
