@@ -1,0 +1,7 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/r3_h; mkdir -p $OUT
+TAG=r3_h/ab VARIANTS="base head" ROUNDS=3 ARGS="--steps 10000 --handler-batch 0" bash scripts/ab.sh; rc=$?
+echo "ab rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
+TAG=r3_h/ab20 VARIANTS="base head" ROUNDS=3 ARGS="--steps 20 --warmup 5 --handler-batch 0" bash scripts/ab.sh; rc=$?
+echo "ab20 rc=$rc" >> $OUT/status.txt
