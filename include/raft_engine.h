@@ -309,14 +309,11 @@ int raft_append_command_batch_dev(raft_engine* e, const int64_t* group, const in
  * key = (seed lo32, seed hi32).  Purposes: */
 #define RAFT_RNG_TIMER        1u  /* sub = replica >> 2, word replica & 3: the replica's
                                      per-step draw, scaled to the election timeout or to
-                                     the backoff (never both in one step); with R % 4 == 1,
-                                     R > 1 (R = 5) the last replica's word is word 3 of the
-                                     RAFT_RNG_HARNESS draw instead                        */
+                                     the backoff (never both in one step)               */
 #define RAFT_RNG_BACKOFF      2u  /* reserved (the backoff shares the timer word)      */
 #define RAFT_RNG_VOTE_DROP    3u  /* sub = src | chunk << 8: 16-bit drop uniforms */
 #define RAFT_RNG_APPEND_DROP  4u  /* sub = src | chunk << 8                        */
-#define RAFT_RNG_HARNESS      5u  /* sub = 0: w0 churn, w1 command, w2 command id,
-                                     w3 the last replica's timer word when R = 5     */
+#define RAFT_RNG_HARNESS      5u  /* sub = 0: w0 churn, w1 command, w2 command id  */
 #define RAFT_RNG_PARTITION    6u  /* c0 = partition window start, sub = 0: w0 mask */
 #define RAFT_RNG_INIT_STEP    0xFFFFFFFFu  /* c0 of the initial timer draws        */
 void raft_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -161,18 +161,13 @@ static void draw4(const ctx_t* x, uint32_t c0, uint32_t purpose, uint32_t sub, u
 }
 /* `(lo..hi).random()` = Random().nextInt(hi - lo + 1) + lo   (Commons.kt:33-34).
  * Per-replica draws share one Philox call per 4 replicas: replica r takes
- * word (r & 3) of Philox(c0, gid, TIMER, r >> 2) -- except that when the last
- * quad would hold a single replica (R % 4 == 1, R > 1: R = 5), that replica
- * takes the unused word 3 of the step's harness draw Philox(c0, gid, HARNESS,
- * 0) (S-9).  The word is scaled to the span by a 32x32->64 multiply-shift. */
+ * word (r & 3) of Philox(c0, gid, purpose, r >> 2); the word is scaled to the
+ * span by a 32x32->64 multiply-shift (S-9). */
 static int32_t draw_range(const ctx_t* x, uint32_t c0, uint32_t purpose, int32_t r, int32_t lo, int32_t hi) {
     uint32_t w[4];
-    const int32_t R = x->o->R;
-    const int in_harness = purpose == RAFT_RNG_TIMER && R % 4 == 1 && R > 1 && r == R - 1;
-    if (in_harness) draw4(x, c0, RAFT_RNG_HARNESS, 0, w);
-    else draw4(x, c0, purpose, (uint32_t)r >> 2, w);
+    draw4(x, c0, purpose, (uint32_t)r >> 2, w);
     uint32_t span = (uint32_t)(hi - lo) + 1u;
-    return lo + (int32_t)(((uint64_t)w[in_harness ? 3 : (r & 3)] * span) >> 32);
+    return lo + (int32_t)(((uint64_t)w[r & 3] * span) >> 32);
 }
 /* w / 2^32 < ppm / 10^6, exactly */
 static int hit32(uint32_t w, uint32_t ppm) {

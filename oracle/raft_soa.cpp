@@ -76,15 +76,10 @@ void draw4(const Step& x, uint32_t c0, uint32_t purpose, uint32_t sub, uint32_t 
     const uint32_t ctr[4] = {c0, x.gid, purpose, sub};
     philox_ref(ctr, x.s->key, w);
 }
-// replica r's timer word (S-9): word r & 3 of Philox(c0, gid, TIMER, r >> 2),
-// or word 3 of the harness draw for the last replica when R % 4 == 1, R > 1
 int32_t draw_range(const Step& x, uint32_t c0, int32_t r, int32_t lo, int32_t hi) {
     uint32_t w[4];
-    const int32_t R = x.s->R;
-    const bool in_harness = R % 4 == 1 && R > 1 && r == R - 1;
-    if (in_harness) draw4(x, c0, RAFT_RNG_HARNESS, 0, w);
-    else draw4(x, c0, RAFT_RNG_TIMER, (uint32_t)r >> 2, w);
-    return lo + (int32_t)(((uint64_t)w[in_harness ? 3 : (r & 3)] * ((uint32_t)(hi - lo) + 1u)) >> 32);
+    draw4(x, c0, RAFT_RNG_TIMER, (uint32_t)r >> 2, w);
+    return lo + (int32_t)(((uint64_t)w[r & 3] * ((uint32_t)(hi - lo) + 1u)) >> 32);
 }
 bool hit32(uint32_t w, uint32_t ppm) { return (uint64_t)w * 1000000ull < ((uint64_t)ppm << 32); }
 bool hit16(uint32_t u, uint32_t ppm) { return (uint64_t)u * 1000000ull < ((uint64_t)ppm << 16); }

@@ -143,7 +143,8 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
     const uint32_t gid = (uint32_t)(p.g0 + g);
     for (int f = 0; f < F_DEV; ++f) p.st[fidx(p, f, idx)] = 0;
     p.st[fidx(p, RAFT_F_VOTED, idx)] = -1;                               // RaftServer.kt:39
-    p.st[fidx(p, RAFT_F_ELECTION_MS, idx)] = scale_range(replica_timer_word(p, RAFT_RNG_INIT_STEP, gid, r), p.emin, p.emax);
+    const u32x4 w = draw(p, RAFT_RNG_INIT_STEP, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
+    p.st[fidx(p, RAFT_F_ELECTION_MS, idx)] = scale_range(word_of(w, r & 3), p.emin, p.emax);
     p.st[fidx(p, RAFT_F_FLAGS, idx)] = (int32_t)FL_ARMED;
     p.ses[idx] = 0;
     p.ses[p.GR + idx] = 0;
@@ -556,7 +557,8 @@ __device__ __forceinline__ void store_rep(const RepState& x, const DevParams& p,
 
 __device__ __forceinline__ void resolve_rep_draw(RepState& x, const DevParams& p, uint32_t t, uint32_t gid, int r) {
     if (x.fl & FL_DRAW) {
-        x.elec = scale_range(replica_timer_word(p, t, gid, r), p.emin, p.emax);
+        const u32x4 w = draw(p, t, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
+        x.elec = scale_range(word_of(w, r & 3), p.emin, p.emax);
         x.fl &= ~FL_DRAW;
     }
 }

@@ -237,13 +237,6 @@ __device__ __forceinline__ bool no_drops(const DevParams& p) {
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
     return philox4x32_10(c0, gid, purpose, sub, p.key0, p.key1);
 }
-// Replica r's timer word of step c0 (S-9), outside the step kernel: word
-// r & 3 of Philox(c0, gid, TIMER, r >> 2); with R % 4 == 1, R > 1 (R = 5) the
-// last replica takes word 3 of the harness draw Philox(c0, gid, HARNESS, 0).
-__device__ __forceinline__ uint32_t replica_timer_word(const DevParams& p, uint32_t c0, uint32_t gid, int r) {
-    if (p.R % 4 == 1 && p.R > 1 && r == p.R - 1) return draw(p, c0, gid, RAFT_RNG_HARNESS, 0).w;
-    return word_of(draw(p, c0, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2)), r & 3);
-}
 
 // Phase timing (diagnostic builds only, -DRAFT_PROFILE_PHASES): s_memtime
 // deltas per step phase, summed per wave in SGPRs and added to a global
@@ -508,21 +501,14 @@ struct Lanes {
     // Per-step Philox jobs (S-9), one per lane of the group, all evaluated in
     // ONE Philox pass of the wave: J_HARNESS, then the NQ timer quads (the
     // per-replica draw word, used by the election timer and the backoff), then
-    // the NCH drop-word chunks of the first leader to tick, of the first
-    // RequestVote sender and (R = 5) of the second.  Jobs that do not fit in R
-    // lanes are drawn on demand.
-    // TIMER_IN_HARNESS (R % 4 == 1, R > 1, i.e. R = 5): the last replica's
-    // timer word is the harness draw's spare word 3 instead of word 0 of a
-    // quad of its own, and that quad's job lane (J_VOTE2) draws the second
-    // RequestVote sender's drop-word chunk instead (NCH == 1 there).
-    static constexpr bool TIMER_IN_HARNESS = R % 4 == 1 && R > 1;
-    static constexpr int NQ = (R + 3) / 4;             // job lanes of the timer quads (Philox calls per 4 replicas)
+    // the NCH drop-word chunks of the first leader to tick and of the first
+    // RequestVote sender.  Jobs that do not fit in R lanes are drawn on demand.
+    static constexpr int NQ = (R + 3) / 4;             // Philox calls per 4-replica quad
     static constexpr int NCH = (R + 2) / 4;            // drop-word chunks per sender: ceil((R - 1) / 4)
-    static constexpr int J_TIMER = 1, J_TICK = 1 + NQ, J_VOTE = 1 + NQ + NCH, J_VOTE2 = NQ;
+    static constexpr int J_TIMER = 1, J_TICK = 1 + NQ, J_VOTE = 1 + NQ + NCH;
     static constexpr bool JOBS = 1 + NQ <= R;          // harness + timer quads fit
     static constexpr bool TICK_JOB = JOBS && J_TICK + NCH <= R;
     static constexpr bool VOTE_JOB = JOBS && J_VOTE + NCH <= R;
-    static constexpr bool VOTE2_JOB = VOTE_JOB && TIMER_IN_HARNESS && NCH == 1;
     // one chunk per sender: a pass of the group's R lanes covers every sender
     static constexpr bool SENDERS_STAGED = NCH == 1;
 
@@ -546,7 +532,7 @@ struct Lanes {
     }
     // the job lanes of the step's Philox pass, and those holding a sender's
     // second drop-word chunk (R > 5)
-    static constexpr uint64_t TIMER_LANES = lanes_in(J_TIMER, VOTE2_JOB ? J_VOTE2 : J_TICK);
+    static constexpr uint64_t TIMER_LANES = lanes_in(J_TIMER, J_TICK);
     static constexpr uint64_t TICK_LANES = lanes_in(J_TICK, J_VOTE);
     static constexpr uint64_t VOTE_LANES = lanes_in(J_VOTE, R);
     static constexpr uint64_t CHUNK1_LANES = lanes_in(J_TICK + 1, J_VOTE) | lanes_in(J_VOTE + 1, R);
@@ -675,7 +661,6 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
     if constexpr (Lanes<R>::JOBS) {
         return c.tw;
     } else {
-        static_assert(!Lanes<R>::TIMER_IN_HARNESS, "R = 5 has the job lanes");
         return word_of(kdraw(p, c.t, c.gid(), RAFT_RNG_TIMER, (uint32_t)(c.r >> 2)), c.r & 3);
     }
 }
@@ -1023,15 +1008,11 @@ struct Stepper {
     // Predicated, called in wave-uniform control flow.
     // mvr: the lanes of groups with a pending sender (the caller's ballot of
     // vtodo != 0); hasl: lanes with lastIndex >= 1 (constant over the phase).
-    // STAGED: the drop words come from LDS rows -- those of job lane fj when
-    // fj >= 0 (wave-uniform: the second sender's job, R = 5, every group of
-    // the round being at its second sender), else stage_sender_chunks' row of
-    // the sender; otherwise from the first sender's job lanes.
     template <bool STAGED = false>
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
                                                       uint32_t& vtodo, uint64_t mvr, uint32_t send, int32_t qt,
                                                       int32_t qli, int32_t qlt, uint64_t gapw, uint64_t hasl,
-                                                      uint32_t fs, int fj = -1) {
+                                                      uint32_t fs) {
         const int r = c.r;
         const int s = ib(mvr) ? __builtin_ctz(vtodo) : 0;
         vtodo &= vtodo - 1u;
@@ -1040,7 +1021,7 @@ struct Stepper {
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
         uint32_t dw;
-        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, fj >= 0 ? fj : s, s);
+        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t mme = lm(r == s);
@@ -1192,10 +1173,6 @@ struct Stepper {
                 purpose = jt ? RAFT_RNG_TIMER : (jk ? RAFT_RNG_APPEND_DROP : (jv ? RAFT_RNG_VOTE_DROP : RAFT_RNG_HARNESS));
                 sub = jt ? (uint32_t)(r - L::J_TIMER) : (jk ? (uint32_t)c.s_tick : (jv ? (uint32_t)c.s_vote : 0u));
                 sub = (sub & 0xFFu) | (ib(L::CHUNK1_LANES) ? 0x100u : 0u);
-            } else if (L::VOTE2_JOB && r == L::J_VOTE2) {                  // the group's second RequestVote sender
-                const uint32_t v2 = vtodo & (vtodo - 1u);
-                purpose = RAFT_RNG_VOTE_DROP;
-                sub = (uint32_t)((v2 ? __builtin_ctz(v2) : -1) & 0xFF);
             } else if (r >= L::J_TIMER && r < L::J_TICK) {
                 purpose = RAFT_RNG_TIMER; sub = (uint32_t)(r - L::J_TIMER);
             } else if (r >= L::J_TICK && r < L::J_VOTE) {
@@ -1218,10 +1195,7 @@ struct Stepper {
             hw1 = h.y;
             hw2 = h.z;
             // every word this lane needs from the jobs, fetched in one batch
-            if constexpr (L::TIMER_IN_HARNESS)                              // the last replica: harness word 3
-                c.tw = c.jl[ib(L::lanes_of(R - 1)) ? (c.base << 2) + 3 : ((c.base + L::J_TIMER) << 2) + r];
-            else
-                c.tw = job_word(c, L::J_TIMER, r);                          // word r & 3 of timer quad r >> 2
+            c.tw = job_word(c, L::J_TIMER, r);                              // word r & 3 of timer quad r >> 2
             if constexpr (L::TICK_JOB) c.dwt = job_drop_word(c, L::J_TICK, c.s_tick);
             if constexpr (L::VOTE_JOB) c.dwv = job_drop_word(c, L::J_VOTE, c.s_vote);
         } else {
@@ -1280,19 +1254,10 @@ struct Stepper {
                 vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                 mv = lm(vtodo != 0);
                 if (mv) {                                                   // groups with 2+ senders
-                    // R = 5: the second sender's chunk is one of the step's
-                    // jobs, so the staging pass waits for a third round
-                    int fj = L::VOTE2_JOB ? L::J_VOTE2 : -1;
-                    if (fj < 0) {
-                        if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                    }
+                    if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
                     do {
-                        vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs, fj);
+                        vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                         mv = lm(vtodo != 0);
-                        if (L::VOTE2_JOB && fj >= 0 && mv) {               // groups with 3+ senders
-                            stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                            fj = -1;
-                        }
                     } while (mv);
                 }
             }
