@@ -79,3 +79,26 @@ def test_default_launch_length_per_kernel_variant():
     assert abi.bench_steps_per_launch(5, abi.MODE_TEXTBOOK) == abi.MAX_STEPS_PER_LAUNCH
     assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 256) == abi.MAX_STEPS_PER_LAUNCH
     assert bench.launch_length(10_000, 400) == 400 and bench.launch_length(20, 400) == 20
+
+
+def test_handler_requests_shapes_and_ranges():
+    """bench.handler_requests: n messages over G x R replicas, vote [n, 4] and
+    append [n, 8] as the structs' 32-bit words, half the appends at prev -1."""
+    import numpy as np
+    rng = np.random.default_rng(0)
+    g, d, v, a = bench.handler_requests(rng, 10_000, 50, 5, 7)
+    assert g.shape == (10_000,) and d.dtype == np.int32 and v.shape == (10_000, 4) and a.shape == (10_000, 8)
+    assert g.min() >= 0 and g.max() < 50 and d.min() >= 0 and d.max() < 5
+    assert v.dtype == np.int32 and a.dtype == np.int32
+    assert 0.45 < float(np.mean(a[:, 2] == -1)) < 0.55
+    assert set(np.unique(v[:, 1])) <= set(range(1, 6))
+
+
+def test_pmc_parse_launches_of_subrange_dispatches():
+    """A launch of the warmup / timed legs is one dispatch per sub-range; the
+    PMC parse sums them, and the trace time is the union of the intervals."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import pmc_parse
+    assert pmc_parse.expand([["warmup", 5, 3], ["timed", 20, 3], ["streaming", 1, 1], ["timed", 7]]) == \
+        [0, 0, 0, 1, 1, 1, 2, 3]
+    assert pmc_parse.union_ms([(0, 10), (5, 20), (30, 40), (35, 38)]) == 30 / 1e6
