@@ -480,6 +480,17 @@ def main(argv=None, result=None):
     import torch
     import torch.distributed as dist
 
+    # RAFT_BENCH_SYNC=spin|yield|blocking: how the host waits in a
+    # synchronisation (hipSetDeviceFlags, before the device is initialised;
+    # unset = the runtime's default).  Measured in DESIGN.md §5.3.
+    sync_mode = os.environ.get("RAFT_BENCH_SYNC")
+    if sync_mode:
+        import ctypes
+        flags = {"spin": 0x1, "yield": 0x2, "blocking": 0x4}[sync_mode]
+        rc = ctypes.CDLL("libamdhip64.so.7").hipSetDeviceFlags(flags)
+        if rc != 0:
+            print(f"bench.py: hipSetDeviceFlags({sync_mode}) returned {rc}", file=sys.stderr, flush=True)
+
     # rehearsal knobs for a one-GPU box (never set by the driver):
     # RAFT_BENCH_BACKEND=gloo with RAFT_BENCH_ONE_DEVICE=1 runs every rank on
     # cuda:0 with gloo collectives, which exercises the N > 1 path end to end
@@ -574,11 +585,10 @@ def main(argv=None, result=None):
                 gcounters[done:done + k].copy_(counters[done:done + k])
                 dist.all_reduce(gcounters[done:done + k])
     ev1.record(stream)
-    eng.sync()
-    torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
+    wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
     if coll:
         dist.barrier()
-    wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
     kern_ms, launches = eng.kernel_time()
     eng.set_kernel_timing(False)
@@ -751,9 +761,12 @@ def main(argv=None, result=None):
         "roofline_valu": roofline_valu,
         "roofline_streaming": streaming,
         "timing": {"wall_ms": wall * 1e3, "stream_event_ms": ev_ms, "step_kernel_ms_total": kern_ms,
-                   "note": "the timed region: wall clock between the barriers/syncs (ms_per_step uses the larger "
-                           "of wall and the stream events around it), and the summed step-kernel launches; the "
-                           "rest is launch latency, the per-launch counter reduction and the final sync"},
+                   "note": "the timed region: each rank's wall clock from after the opening barrier + device "
+                           "sync to after its closing device sync (the closing barrier follows the clock; the job's "
+                           "time is the MAX over ranks), ms_per_step uses the larger of wall and the stream events "
+                           "around the launches; step_kernel_ms_total is the time during which a step kernel ran "
+                           "(the union of the sub-range launches); the rest is launch latency, the counter "
+                           "reductions, the counter all-reduce (N > 1) and the final sync"},
         "valid": overflow == 0 and wmiss == 0 and bad_untimed == 0,
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
