@@ -480,17 +480,6 @@ def main(argv=None, result=None):
     import torch
     import torch.distributed as dist
 
-    # RAFT_BENCH_SYNC=spin|yield|blocking: how the host waits in a
-    # synchronisation (hipSetDeviceFlags, before the device is initialised;
-    # unset = the runtime's default).  Measured in DESIGN.md §5.3.
-    sync_mode = os.environ.get("RAFT_BENCH_SYNC")
-    if sync_mode:
-        import ctypes
-        flags = {"spin": 0x1, "yield": 0x2, "blocking": 0x4}[sync_mode]
-        rc = ctypes.CDLL("libamdhip64.so.7").hipSetDeviceFlags(flags)
-        if rc != 0:
-            print(f"bench.py: hipSetDeviceFlags({sync_mode}) returned {rc}", file=sys.stderr, flush=True)
-
     # rehearsal knobs for a one-GPU box (never set by the driver):
     # RAFT_BENCH_BACKEND=gloo with RAFT_BENCH_ONE_DEVICE=1 runs every rank on
     # cuda:0 with gloo collectives, which exercises the N > 1 path end to end
@@ -550,15 +539,27 @@ def main(argv=None, result=None):
     wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
 
     # ---- warmup (untimed) ----
+    comm_stream = torch.cuda.Stream(device=dev)
     if args.warmup:
         eng.step_async(args.warmup, wcount.data_ptr())
+    if coll:
+        # the counter all-reduce's first use on its stream (communicator
+        # and stream setup) belongs to the warmup: the warmup rows, all-reduced
+        # exactly as the timed chunks are, twice
+        wev = torch.cuda.Event()
+        wev.record(stream)
+        comm_stream.wait_event(wev)
+        wglob = torch.zeros_like(wcount)
+        with torch.cuda.stream(comm_stream):
+            for _ in range(2):
+                wglob.copy_(wcount)
+                dist.all_reduce(wglob)
     eng.sync()
     torch.cuda.synchronize(dev)
     if coll:
         dist.barrier()
 
     # ---- timed region ----
-    comm_stream = torch.cuda.Stream(device=dev)
     eng.set_kernel_timing(True)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
