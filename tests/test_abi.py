@@ -111,3 +111,17 @@ def test_write_log_rejects_wrong_shapes():
         e.write_log(np.zeros((2, 3, 8), np.int32), np.zeros((2, 3, 4), np.uint32))
     with pytest.raises(ValueError):
         e.write_log(np.zeros((2, 2, 8), np.int32), np.zeros((2, 2, 8), np.uint32))
+
+
+def test_missing_entry_points_bind_stubs(monkeypatch):
+    """An experimental library (RAFT_ENGINE_LIB) without some entry point gets a
+    warning per missing symbol and a stub that raises a clear error when called
+    (here: the oracle's library, which exports none of the engine's symbols)."""
+    other = os.path.join(ROOT, "oracle", "lib", "liboracle.so")
+    if not os.path.exists(other):
+        pytest.skip("oracle library not built")
+    monkeypatch.setenv("RAFT_ENGINE_LIB", other)
+    with pytest.warns(UserWarning, match="raft_engine_subranges"):
+        lib = abi.load_library(other)
+    with pytest.raises(RuntimeError, match="not in this engine build"):
+        lib.raft_engine_subranges(None)
