@@ -4,14 +4,18 @@ intervals (launch sub-ranges overlap), divided by the number of full-grid
 K-step launches (dispatches / sub-ranges), next to the plain per-dispatch
 average that rocprofv3 --stats reports.
 
-    python scripts/trace_union.py <dir with *kernel_trace.csv> [subranges] [first_n_launches]"""
+    python scripts/trace_union.py <dir with *kernel_trace.csv> [subranges] [launches] [skip_dispatches]
+
+launches / skip_dispatches select the timed launches of a bench run: e.g. the
+default run's trace is 3 warmup dispatches, then 25 timed launches x 3, then
+the streaming leg: `... 3 25 3`."""
 import csv
 import glob
 import json
 import sys
 
 
-def main(d, nsub=None, first=None):
+def main(d, nsub=None, first=None, skip=0):
     rows = []
     for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -19,6 +23,7 @@ def main(d, nsub=None, first=None):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id"),
                              int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)))
     rows.sort()
+    rows = rows[skip:]
     streams = sorted({r[2] for r in rows})
     nsub = nsub or len(streams)
     if first:
@@ -42,4 +47,5 @@ def main(d, nsub=None, first=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None, int(sys.argv[3]) if len(sys.argv) > 3 else None)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None, int(sys.argv[3]) if len(sys.argv) > 3 else None,
+         int(sys.argv[4]) if len(sys.argv) > 4 else 0)
