@@ -227,7 +227,13 @@ int raft_engine_step(raft_engine* e, int32_t n_steps, int64_t* counters_host);
  * DEVICE pointer to [n_steps][RAFT_COUNTER_STRIDE] int64 (overwritten). */
 int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_dev);
 int raft_engine_sync(raft_engine* e);
-/* hipStream_t of the engine, as void* (for event timing by the caller). */
+/* hipStream_t of the engine, as void* (for event timing by the caller).  Work
+ * enqueued on it after a step_async sees that call's steps finished (state,
+ * logs and counter rows).  With launch sub-ranges the step kernels run on the
+ * engine's own side streams, which wait for this stream only where an engine
+ * call other than a step enqueued work on it: caller work on this stream is
+ * ordered before the counter reductions of later steps, not before their
+ * step kernels (which touch only engine memory). */
 void*   raft_engine_stream(raft_engine* e);
 /* Kernel timing: while enabled, every step-kernel launch (of every
  * sub-range) carries its own start / stop timestamps.  raft_engine_kernel_time()
