@@ -710,6 +710,8 @@ struct raft_engine {
     char* hst;
     size_t hst_bytes;
     unsigned int* bflags_host;
+    char* aux;                  // device staging of the state / log / digest accessors, grow-only
+    size_t aux_bytes;
     int64_t* counters_dev;      // [K][STRIDE] scratch
     int nchunks;                // counter-reduction chunks of REDUCE_CHUNK partials
     unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
@@ -860,6 +862,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->bst = e->bio = e->hst = nullptr;
     e->bst_bytes = e->bio_bytes = e->hst_bytes = 0;
     e->bflags_host = nullptr;
+    e->aux = nullptr;
+    e->aux_bytes = 0;
     e->device = device;
     e->t = 0;
     const int64_t G = p->G, R = p->R;
@@ -974,6 +978,7 @@ int raft_engine_destroy(raft_engine* e) {
     if (e->bio) (void)hipFree(e->bio);
     if (e->hst) (void)hipHostFree(e->hst);
     if (e->bflags_host) (void)hipHostFree(e->bflags_host);
+    if (e->aux) (void)hipFree(e->aux);
     (void)hipFree(e->base);
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1162,6 +1167,30 @@ int raft_engine_set_step_index(raft_engine* e, int64_t t) {
 }
 int64_t raft_engine_device_bytes(raft_engine* e) { return e ? (int64_t)e->bytes : -1; }
 
+// Grow-only engine staging (the batch path, the state / log / digest accessors) (no allocation, and so no
+// device-wide hipFree synchronisation, once a batch size has been seen).
+static int grow_dev(raft_engine* e, char** buf, size_t* have, size_t need) {
+    if (need <= *have) return RAFT_OK;
+    if (*buf) HIP_TRY(hipFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    need = std::max(need, (size_t)1 << 20) * 5 / 4;
+    HIP_TRY(hipMalloc((void**)buf, need));
+    *have = need;
+    return RAFT_OK;
+}
+static int grow_host(raft_engine* e, char** buf, size_t* have, size_t need) {
+    if (need <= *have) return RAFT_OK;
+    if (*buf) HIP_TRY(hipHostFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    need = std::max(need, (size_t)1 << 20) * 5 / 4;
+    HIP_TRY(hipHostMalloc((void**)buf, need, hipHostMallocDefault));
+    *have = need;
+    return RAFT_OK;
+}
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 static int check_range(raft_engine* e, int64_t g0, int64_t n) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     if (g0 < 0 || n < 0 || g0 + n > e->p.G) return fail(RAFT_ERANGE, "group range outside the engine");
@@ -1175,12 +1204,11 @@ int raft_engine_read_state(raft_engine* e, int64_t g0, int64_t n, int32_t* out) 
     HIP_TRY(hipSetDevice(e->device));
     e->fork_needed = true;
     const size_t bytes = (size_t)n * raft_group_words(e->p.R) * 4;
-    int32_t* buf = nullptr;
-    HIP_TRY(hipMalloc(&buf, bytes));
+    if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, bytes)) return rc;
+    int32_t* buf = (int32_t*)e->aux;
     dispatch_R<PackL>(e->p.R, e, g0, n, buf);
     hipError_t err = hipMemcpyAsync(out, buf, bytes, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-    (void)hipFree(buf);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
     return RAFT_OK;
 }
@@ -1199,15 +1227,14 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
     HIP_TRY(hipSetDevice(e->device));
     e->fork_needed = true;
     const size_t bytes = (size_t)n * W * 4;
-    int32_t* buf = nullptr;
-    HIP_TRY(hipMalloc(&buf, bytes));
+    if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, bytes)) return rc;
+    int32_t* buf = (int32_t*)e->aux;
     hipError_t err = hipMemcpyAsync(buf, in, bytes, hipMemcpyHostToDevice, e->stream);
     e->cache_valid = false;
     if (err == hipSuccess) {
         dispatch_R<UnpackL>(e->p.R, e, g0, n, buf);
         err = hipStreamSynchronize(e->stream);
     }
-    (void)hipFree(buf);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
     return RAFT_OK;
 }
@@ -1216,8 +1243,8 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
 static int log_image(raft_engine* e, int64_t g0, int64_t n, std::vector<uint2>& tmp, bool to_ring) {
     e->fork_needed = true;
     const size_t cnt = (size_t)n * e->p.R * e->p.log_cap;
-    uint2* buf = nullptr;
-    HIP_TRY(hipMalloc(&buf, cnt * 8));
+    if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, cnt * 8)) return rc;
+    uint2* buf = (uint2*)e->aux;
     hipError_t err = hipSuccess;
     if (to_ring) err = hipMemcpyAsync(buf, tmp.data(), cnt * 8, hipMemcpyHostToDevice, e->stream);
     if (err == hipSuccess) {
@@ -1227,7 +1254,6 @@ static int log_image(raft_engine* e, int64_t g0, int64_t n, std::vector<uint2>& 
     }
     if (err == hipSuccess && !to_ring) err = hipMemcpyAsync(tmp.data(), buf, cnt * 8, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-    (void)hipFree(buf);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
     return RAFT_OK;
 }
@@ -1268,15 +1294,14 @@ int raft_engine_digest_range(raft_engine* e, int64_t g0, int64_t n, uint64_t* ou
     if (n == 0) return RAFT_OK;
     HIP_TRY(hipSetDevice(e->device));
     e->fork_needed = true;
-    unsigned long long* d = nullptr;
-    HIP_TRY(hipMalloc(&d, 8));
+    if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, 8)) return rc;
+    unsigned long long* d = (unsigned long long*)e->aux;
     hipError_t err = hipMemsetAsync(d, 0, 8, e->stream);
     if (err == hipSuccess) {
         dispatch_R<DigestL>(e->p.R, e, g0, n, d);
         err = hipMemcpyAsync(out, d, 8, hipMemcpyDeviceToHost, e->stream);
     }
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-    (void)hipFree(d);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
     return RAFT_OK;
 }
@@ -1288,8 +1313,8 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
     e->fork_needed = true;
     *mismatched = 0;
     if (n == 0) return RAFT_OK;
-    void* d = nullptr;
-    HIP_TRY(hipMalloc(&d, 8 + (flags ? (size_t)n : 0)));
+    if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, 8 + (flags ? (size_t)n : 0))) return rc;
+    void* d = e->aux;
     unsigned long long* cnt = (unsigned long long*)d;
     uint8_t* fl = flags ? (uint8_t*)d + 8 : nullptr;
     unsigned long long h = 0;
@@ -1301,35 +1326,11 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
     if (err == hipSuccess) err = hipMemcpyAsync(&h, cnt, 8, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess && flags) err = hipMemcpyAsync(flags, fl, (size_t)n, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
-    (void)hipFree(d);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
     *mismatched = (int64_t)h;
     return RAFT_OK;
 }
 
-// Grow-only engine staging of the batch path (no allocation, and so no
-// device-wide hipFree synchronisation, once a batch size has been seen).
-static int grow_dev(raft_engine* e, char** buf, size_t* have, size_t need) {
-    if (need <= *have) return RAFT_OK;
-    if (*buf) HIP_TRY(hipFree(*buf));
-    *buf = nullptr;
-    *have = 0;
-    need = std::max(need, (size_t)1 << 20) * 5 / 4;
-    HIP_TRY(hipMalloc((void**)buf, need));
-    *have = need;
-    return RAFT_OK;
-}
-static int grow_host(raft_engine* e, char** buf, size_t* have, size_t need) {
-    if (need <= *have) return RAFT_OK;
-    if (*buf) HIP_TRY(hipHostFree(*buf));
-    *buf = nullptr;
-    *have = 0;
-    need = std::max(need, (size_t)1 << 20) * 5 / 4;
-    HIP_TRY(hipHostMalloc((void**)buf, need, hipHostMallocDefault));
-    *have = need;
-    return RAFT_OK;
-}
-static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // The batch on device buffers: keys, a stable radix sort over the key bits,
 // the handlers; one synchronisation at the end for the status flags.
