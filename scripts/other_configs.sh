@@ -7,8 +7,11 @@ run() {
   rc=$?; echo "$* rc=$rc" >> "$OUT/status.txt"; [ $rc -ne 0 ] && { cat "$OUT/b.log"; exit $rc; }
   grep '^{' "$OUT/b.log" | tail -1 >> "$OUT/bench_other_configs.jsonl"
 }
-run --config 5 --groups 100000
-run --mode textbook
-run --config 5 --groups 100000 --mode textbook
-run --config 2 --groups 10000 --steps 1000
+run --config 5 --groups 100000 --handler-batch 0
+run --mode textbook --handler-batch 0
+run --mode textbook --ae-max-entries 8 --handler-batch 0
+run --config 5 --groups 100000 --mode textbook --handler-batch 0
+run --config 2 --groups 10000 --steps 1000 --handler-batch 0
+run --groups 125000 --handler-batch 0
+run --groups 250000 --handler-batch 0
 exit 0
