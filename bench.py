@@ -11,14 +11,19 @@ all state resident in HBM before the timed region starts.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Multi-GPU (BASELINE.json configs[3], "config 4"): one process per GPU.  With
---gpus N > 1 and no torch.distributed environment, this script spawns the N
-rank processes itself (fresh interpreters; the parent makes no HIP or
-torch.cuda call) and exits with their status.  By default the 10^6 groups are
-split into contiguous global-id ranges (strong scaling); --scaling weak gives
-every GPU its own 10^6 groups.  Groups never talk across GPUs, so the only
-collective is the all-reduce of the per-step counter rows over RCCL, batched
-on a side stream.  Rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU.  With --gpus N > 1 and no torch.distributed
+environment, this script spawns the N rank processes itself (fresh
+interpreters; the parent makes no HIP or torch.cuda call) and exits with their
+status.  Groups never talk across GPUs, so the path shards with no data-path
+exchange: by default every GPU runs its own 10^6 groups (weak scaling,
+contiguous global-id ranges, `value` = every rank's group-steps / the MAX of
+the ranks' times).  The line then also carries `config4_strong`, BASELINE.json
+configs[3] measured in the same job: 10^6 groups split into contiguous
+global-id ranges over the N GPUs, timed the same way, whose all-reduced
+counter rows must equal rank 0's weak-shard rows (the same global groups).
+--scaling strong makes that split the main measurement.  The only collective is
+the all-reduce of the per-step counter rows over RCCL, batched on a side
+stream.  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -241,7 +246,11 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--groups", type=int, default=1_000_000,
                     help="total groups (strong scaling) or groups per GPU (weak scaling)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: --groups per GPU (the path shards with no exchange); strong: --groups split over "
+                         "the GPUs (config 4)")
+    ap.add_argument("--no-strong-leg", action="store_true",
+                    help="N > 1, weak scaling: skip the config-4 strong-shard leg")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
                     help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
@@ -440,6 +449,136 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
     return out
 
 
+def timed_leg(eng, args, chunk, coll, dev, world):
+    """Warmup (untimed), then the timed region of `args.steps` lockstep steps on
+    `eng`: enqueued in chunks of `chunk` steps, each chunk's counter rows
+    all-reduced on a side stream when `coll`, bracketed by a barrier and a
+    device sync on both sides.  Returns this rank's clock, the stream-event and
+    step-kernel times, the job's elapsed time (MAX over ranks) and the counter
+    rows (this rank's, all ranks', warmup)."""
+    import torch
+    import torch.distributed as dist
+    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
+    counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+    gcounters = torch.zeros_like(counters) if coll else counters
+    wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+
+    # ---- warmup (untimed) ----
+    comm_stream = torch.cuda.Stream(device=dev)
+    if args.warmup:
+        eng.step_async(args.warmup, wcount.data_ptr())
+    if coll:
+        # the counter all-reduce's first use on its stream (communicator
+        # and stream setup) belongs to the warmup: the warmup rows, all-reduced
+        # exactly as the timed chunks are, twice
+        wev = torch.cuda.Event()
+        wev.record(stream)
+        comm_stream.wait_event(wev)
+        wglob = torch.zeros_like(wcount)
+        with torch.cuda.stream(comm_stream):
+            for _ in range(2):
+                wglob.copy_(wcount)
+                dist.all_reduce(wglob)
+    eng.sync()
+    torch.cuda.synchronize(dev)
+    if coll:
+        dist.barrier()
+
+    # ---- timed region ----
+    eng.set_kernel_timing(True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    # the chunks' counter rows and events, made before the clock starts (torch
+    # tensor indexing in the loop put ~80 us of host time ahead of the first
+    # launch, 6 % of the driver's 20-step run)
+    plan = [(q, min(chunk, args.steps - q)) for q in range(0, args.steps, chunk)]
+    rows = [counters[q].data_ptr() for q, _ in plan]
+    chunk_ev = [torch.cuda.Event() for _ in plan] if coll else []
+    torch.cuda.synchronize(dev)
+    if coll:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for ci, (done, k) in enumerate(plan):
+        eng.step_async(k, rows[ci])
+        if coll:
+            # the only collective: the batched per-step counter all-reduce,
+            # off the critical path on a side stream (counters never feed
+            # back); this rank's own rows stay in `counters`
+            chunk_ev[ci].record(stream)
+            comm_stream.wait_event(chunk_ev[ci])
+            with torch.cuda.stream(comm_stream):
+                gcounters[done:done + k].copy_(counters[done:done + k])
+                dist.all_reduce(gcounters[done:done + k])
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
+    wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
+    if coll:
+        dist.barrier()
+    ev_ms = ev0.elapsed_time(ev1)
+    kern_ms, launches = eng.kernel_time()
+    eng.set_kernel_timing(False)
+
+    elapsed = max(wall, ev_ms / 1e3)
+    kern_avg_ms = kern_ms / max(1, launches)
+    if coll:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ka = torch.tensor([kern_avg_ms], dtype=torch.float64, device=dev)
+        kall = [torch.zeros_like(ka) for _ in range(world)]
+        dist.all_gather(kall, ka)
+        kern_avg_per_rank = [float(x.item()) for x in kall]
+    else:
+        kern_avg_per_rank = [kern_avg_ms]
+    return {"wall": wall, "ev_ms": ev_ms, "kern_ms": kern_ms, "launches": launches, "elapsed": elapsed,
+            "kern_avg_ms": kern_avg_ms, "kern_avg_per_rank": kern_avg_per_rank,
+            "counters": counters, "gcounters": gcounters, "wcount": wcount}
+
+
+def strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, weak_rows0):
+    """BASELINE.json configs[3] (config 4) inside an N > 1 weak-scaling job:
+    --groups groups split into contiguous global-id ranges over the ranks,
+    warmed up and timed exactly like the main leg (timed_leg).  Rank 0's weak
+    shard holds the same global groups 0..groups-1, so the strong leg's
+    all-reduced counter rows must equal rank 0's weak rows (`weak_rows0`)."""
+    eng_mod = importlib.import_module("raft-kotlin_amd.engine")
+    import torch
+    R = kw["R"]
+    g0, G = shard(args.groups, world, rank, "strong")
+    per_rank = [shard(args.groups, world, q, "strong")[1] for q in range(world)]
+    flat = -(-G // (64 // R)) * 64 * log_cap * 8
+    window = 0 if flat <= 0.6 * torch.cuda.get_device_properties(dev).total_memory else 256
+    params = abi.make_params(log_cap=max(log_cap, window), log_window=window, steps_per_launch=L, mode=mode,
+                             subranges=args.subranges or (1 if args.steps <= L else 0),
+                             ae_max_entries=args.ae_max_entries, **dict(kw, G=G, g0=g0))
+    eng = eng_mod.RaftEngine(params, device=local)
+    nsub = eng.subranges
+    try:
+        leg = timed_leg(eng, args, chunk, coll, dev, world)
+    finally:
+        eng.close()
+    c_all = leg["gcounters"].cpu().numpy()[:, : abi.NUM_COUNTERS]
+    wc = leg["wcount"].cpu().numpy()[: args.warmup, : abi.NUM_COUNTERS]
+    bad = int(c_all[:, abi.C_INDEX["log_overflow"]].sum() + c_all[:, abi.C_INDEX["log_window_miss"]].sum()
+              + wc[:, abi.C_INDEX["log_overflow"]].sum() + wc[:, abi.C_INDEX["log_window_miss"]].sum())
+    out = {"value": args.groups * args.steps / leg["elapsed"], "unit": "group-steps/s", "scaling": "strong",
+           "ms_per_step": leg["elapsed"] * 1e3 / args.steps, "groups_total": args.groups, "groups_per_rank": per_rank,
+           "steps_per_launch": L, "subranges": nsub, "log_window": window,
+           "step_waves_per_rank": -(-G // (64 // R)),
+           "grid_fill": grid_fill(G, R, L, abi.bench_steps_per_launch(R, mode, window) < abi.MAX_STEPS_PER_LAUNCH),
+           "kernel_avg_ms_per_rank": leg["kern_avg_per_rank"],
+           "timing": {"wall_ms": leg["wall"] * 1e3, "stream_event_ms": leg["ev_ms"],
+                      "step_kernel_ms_total": leg["kern_ms"]},
+           "valid": bad == 0,
+           "note": "config 4 in the same job: the groups split by contiguous global id over the GPUs, the same "
+                   "steps, warmup and timing as the main leg; counters_equal_rank0_weak_shard: its all-reduced "
+                   "per-step counter rows equal rank 0's weak-leg rows, which cover the same global groups"}
+    if weak_rows0 is not None:
+        out["counters_equal_rank0_weak_shard"] = bool(np.array_equal(c_all, weak_rows0))
+    return out
+
+
 def plan_only(args, world, rank):
     """The rank/shard plumbing without a GPU (tests/test_bench_cpu.py)."""
     import torch
@@ -533,79 +672,10 @@ def main(argv=None, result=None):
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs
-    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
-    counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
-    gcounters = torch.zeros_like(counters) if coll else counters
-    wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
-
-    # ---- warmup (untimed) ----
-    comm_stream = torch.cuda.Stream(device=dev)
-    if args.warmup:
-        eng.step_async(args.warmup, wcount.data_ptr())
-    if coll:
-        # the counter all-reduce's first use on its stream (communicator
-        # and stream setup) belongs to the warmup: the warmup rows, all-reduced
-        # exactly as the timed chunks are, twice
-        wev = torch.cuda.Event()
-        wev.record(stream)
-        comm_stream.wait_event(wev)
-        wglob = torch.zeros_like(wcount)
-        with torch.cuda.stream(comm_stream):
-            for _ in range(2):
-                wglob.copy_(wcount)
-                dist.all_reduce(wglob)
-    eng.sync()
-    torch.cuda.synchronize(dev)
-    if coll:
-        dist.barrier()
-
-    # ---- timed region ----
-    eng.set_kernel_timing(True)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    # the chunks' counter rows and events, made before the clock starts (torch
-    # tensor indexing in the loop put ~80 us of host time ahead of the first
-    # launch, 6 % of the driver's 20-step run)
-    plan = [(q, min(chunk, args.steps - q)) for q in range(0, args.steps, chunk)]
-    rows = [counters[q].data_ptr() for q, _ in plan]
-    chunk_ev = [torch.cuda.Event() for _ in plan] if coll else []
-    torch.cuda.synchronize(dev)
-    if coll:
-        dist.barrier()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for ci, (done, k) in enumerate(plan):
-        eng.step_async(k, rows[ci])
-        if coll:
-            # the only collective: the batched per-step counter all-reduce,
-            # off the critical path on a side stream (counters never feed
-            # back); this rank's own rows stay in `counters`
-            chunk_ev[ci].record(stream)
-            comm_stream.wait_event(chunk_ev[ci])
-            with torch.cuda.stream(comm_stream):
-                gcounters[done:done + k].copy_(counters[done:done + k])
-                dist.all_reduce(gcounters[done:done + k])
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
-    wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
-    if coll:
-        dist.barrier()
-    ev_ms = ev0.elapsed_time(ev1)
-    kern_ms, launches = eng.kernel_time()
-    eng.set_kernel_timing(False)
-
-    elapsed = max(wall, ev_ms / 1e3)
-    kern_avg_ms = kern_ms / max(1, launches)
-    if coll:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        ka = torch.tensor([kern_avg_ms], dtype=torch.float64, device=dev)
-        kall = [torch.zeros_like(ka) for _ in range(world)]
-        dist.all_gather(kall, ka)
-        kern_avg_per_rank = [float(x.item()) for x in kall]
-    else:
-        kern_avg_per_rank = [kern_avg_ms]
+    leg = timed_leg(eng, args, chunk, coll, dev, world)
+    wall, ev_ms, kern_ms, launches = leg["wall"], leg["ev_ms"], leg["kern_ms"], leg["launches"]
+    elapsed, kern_avg_ms, kern_avg_per_rank = leg["elapsed"], leg["kern_avg_ms"], leg["kern_avg_per_rank"]
+    counters, gcounters, wcount = leg["counters"], leg["gcounters"], leg["wcount"]
 
     c_all = gcounters.cpu().numpy()[:, : abi.NUM_COUNTERS]    # all ranks' groups
     c_loc = counters.cpu().numpy()[:, : abi.NUM_COUNTERS]     # this rank's groups (before the all-reduce)
@@ -709,6 +779,14 @@ def main(argv=None, result=None):
                 "properties); over the timed steps, Log Matching at the end of the run",
     }
 
+    # config 4 (the 10^6 groups split over the GPUs) beside a weak-scaling job
+    strong = None
+    if world > 1 and args.scaling == "weak" and args.config == 3 and not args.no_strong_leg:
+        eng.close()
+        eng = None
+        strong = strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk,
+                            c_loc if rank == 0 else None)
+
     cfg_name = "config4" if world > 1 and args.config == 3 and args.scaling == "strong" else f"config{args.config}"
     out = {
         "metric": METRIC,
@@ -724,8 +802,11 @@ def main(argv=None, result=None):
         "dtype": "int32",
         "data": "synthetic (seeded Philox harness: drops, churn, commands)",
         "config": {
-            "workload": f"{cfg_name}: {total_groups} groups x {R} replicas"
-                        + (f" sharded by contiguous group id over {world} GPUs" if world > 1 else "")
+            "workload": (f"{cfg_name}: {total_groups} groups x {R} replicas"
+                         + (f" sharded by contiguous group id over {world} GPUs" if world > 1 else "")
+                         if world == 1 or args.scaling == "strong" else
+                         f"{cfg_name} on every GPU (weak scaling): {G_local} groups x {R} replicas per GPU, "
+                         f"{world} GPUs, {total_groups} groups in contiguous global-id ranges")
                         + {3: ", 5% drop, leader-isolation churn 1e-3 x 15 steps, 1/4 command per group-step",
                            5: ", 2-way partitions 25 of every 50 steps, 1 command per step to every leader",
                            2: ", no faults, 1/4 command per group-step"}[args.config]
@@ -772,6 +853,8 @@ def main(argv=None, result=None):
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
+    if strong is not None:
+        out["config4_strong"] = strong
     if args.handler_batch > 0 and world == 1 and not coll:
         out["handler_batch"] = handler_batch_leg(eng, args, dict(kw, mode=mode, ae_max_entries=args.ae_max_entries),
                                                  log_cap, dev, G_local, R)
@@ -783,7 +866,8 @@ def main(argv=None, result=None):
     if result is not None:
         result.update(out=out, counters_all=c_all, counters_local=c_loc,
                       warmup_counters=wcount.cpu().numpy()[: args.warmup, : abi.NUM_COUNTERS])
-    eng.close()
+    if eng is not None:
+        eng.close()
     if coll:
         dist.destroy_process_group()
     return 0
