@@ -672,6 +672,7 @@ def main(argv=None, result=None):
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs
+    hbm_bytes_engine = eng.device_bytes
     leg = timed_leg(eng, args, chunk, coll, dev, world)
     wall, ev_ms, kern_ms, launches = leg["wall"], leg["ev_ms"], leg["kern_ms"], leg["launches"]
     elapsed, kern_avg_ms, kern_avg_per_rank = leg["elapsed"], leg["kern_avg_ms"], leg["kern_avg_per_rank"]
@@ -813,7 +814,7 @@ def main(argv=None, result=None):
                         + (", textbook mode" if mode else "")
                         + (f", up to {args.ae_max_entries} entries per AppendEntries" if args.ae_max_entries > 1 else ""),
             "groups_total": total_groups, "groups_per_rank": groups_per_rank, "replicas": R, "log_cap": log_cap,
-            "log_window": window, "hbm_bytes_engine": eng.device_bytes,
+            "log_window": window, "hbm_bytes_engine": hbm_bytes_engine,
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
             "subranges": nsub,
             "step_waves_per_rank": -(-G_local // (64 // R)),
