@@ -511,14 +511,6 @@ struct Lanes {
     static constexpr bool VOTE_JOB = JOBS && J_VOTE + NCH <= R;
     // one chunk per sender: a pass of the group's R lanes covers every sender
     static constexpr bool SENDERS_STAGED = NCH == 1;
-    // Spare lanes: the wave's lanes past its GPW whole groups (4 at R = 5)
-    // hold no replica, but they run the step's Philox pass with the others.
-    // Where the jobs hold the first RequestVote sender's chunk, they draw the
-    // SECOND sender's chunk of up to NSPARE groups with 2+ senders, so the
-    // second vote round reads it there instead of a staging pass.
-    static constexpr int NSPARE = 64 - GPW * R;
-    static constexpr bool SPARE_VOTE2 = NSPARE > 0 && SENDERS_STAGED && JOBS && J_VOTE + NCH <= R;
-    static constexpr uint64_t SPARE_LANES = NSPARE > 0 ? ~0ull << (GPW * R) : 0ull;
 
     // lanes whose replica index is s (compile-time masks)
     // lanes whose replica index is <= s
@@ -563,7 +555,6 @@ struct Ctx {
     uint32_t* tl;             // the wave's vote-tally words, [16] (one per group at base >> 2, R >= 4)
     uint32_t lead;            // the group's LEADER bits at the end of the last step (loop-carried)
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
-    uint32_t spare2;          // LDS word of this group's spare-lane row (Lanes::SPARE_VOTE2, vote round 2)
     PhaseClock clk;
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
     uint2* lr;                // this replica's log row: slot 0 (its wave's block, its lane)
@@ -1017,9 +1008,7 @@ struct Stepper {
     // Predicated, called in wave-uniform control flow.
     // mvr: the lanes of groups with a pending sender (the caller's ballot of
     // vtodo != 0); hasl: lanes with lastIndex >= 1 (constant over the phase).
-    // STAGED: 0 the job's chunk or a direct draw, 1 stage_sender_chunks' rows,
-    // 2 this group's spare-lane row (Lanes::SPARE_VOTE2, the second sender)
-    template <int STAGED = 0>
+    template <bool STAGED = false>
     __device__ __forceinline__ static void vote_round(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt,
                                                       uint32_t& vtodo, uint64_t mvr, uint32_t send, int32_t qt,
                                                       int32_t qli, int32_t qlt, uint64_t gapw, uint64_t hasl,
@@ -1032,8 +1021,7 @@ struct Stepper {
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
         uint32_t dw;
-        if constexpr (STAGED == 2) dw = no_drops(p) ? 0u : c.jl[c.spare2 + dec_if(r, lm(r > s))];   // spare-lane chunk
-        else if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);    // stage_sender_chunks
+        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
         else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t mme = lm(r == s);
@@ -1196,29 +1184,7 @@ struct Stepper {
             // every lane's constant purpose and keeps those products in VGPRs
             // across the step loop (R = 7 spilled them to scratch)
             asm volatile("" : "+v"(purpose));
-            uint32_t gid = c.gid();
-            if constexpr (L::SPARE_VOTE2) {
-                // the spare lanes draw the second RequestVote sender's chunk of
-                // the wave's first NSPARE groups with 2+ senders: the last lane
-                // of each such group posts (gid, sender) to the row of spare
-                // lane GPW * R + rank (rank: such groups below it), which reads
-                // its own row (a wave's LDS operations complete in order)
-                const uint64_t m2 = lm((vtodo & (vtodo - 1u)) != 0u) & L::lanes_of(R - 1);
-                if (m2 && !no_drops(p)) {                                   // wave-uniform
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
-                    const uint32_t row = (uint32_t)(L::GPW * R + rank) << 2;
-                    if (ib(m2 & lm(rank < (uint32_t)L::NSPARE)))
-                        *(uint2*)&c.jl[row] = make_uint2(gid, (uint32_t)__builtin_ctz(vtodo & (vtodo - 1u)));
-                    asm volatile("" ::: "memory");
-                    const uint2 w = *(const uint2*)&c.jl[(c.base + c.r) << 2];
-                    const bool sp = ib(L::SPARE_LANES);
-                    purpose = sp ? (uint32_t)RAFT_RNG_VOTE_DROP : purpose;
-                    sub = sp ? w.y : sub;
-                    gid = sp ? w.x : gid;
-                }
-            }
-            c.job = kdraw(p, c.t, gid, purpose, sub);
+            c.job = kdraw(p, c.t, c.gid(), purpose, sub);
             // stage the wave's jobs in LDS (one ds_write_b128 per lane); a
             // wave's LDS accesses complete in order, so its reads below see
             // them, and the previous step's reads were issued before this write
@@ -1287,20 +1253,7 @@ struct Stepper {
             } else {
                 vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                 mv = lm(vtodo != 0);
-                if constexpr (L::SPARE_VOTE2) {
-                    // the second round from the spare lanes' rows when they hold
-                    // the second sender of every group that has one (mv: the
-                    // lanes of exactly the groups with 2+ senders)
-                    if (mv && __popcll(mv) <= L::NSPARE * R) {              // wave-uniform
-                        const uint64_t m2 = mv & L::lanes_of(R - 1);
-                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32),
-                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0u));
-                        c.spare2 = (uint32_t)(L::GPW * R + rank) << 2;
-                        vote_round<2>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
-                        mv = lm(vtodo != 0);
-                    }
-                }
-                if (mv) {                                                   // groups with 2+ (3+) senders
+                if (mv) {                                                   // groups with 2+ senders
                     if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
                     do {
                         vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
