@@ -177,7 +177,9 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 #ifndef RAFT_STEP_WAVES_PER_EU
 #define RAFT_STEP_WAVES_PER_EU(R, TB, RING) ((!(TB) && !(RING) && (R) <= 5) ? 7 : 6)
 #endif
-template <int R, bool TB, bool RING>
+// NET: the network faults the kernel is built for (raft_step.h NET_DROP /
+// NET_PART; the host's step_fn picks it from raft_params).
+template <int R, bool TB, bool RING, int NET>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU(R, TB, RING))))
 void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     using L = Lanes<R>;
@@ -236,21 +238,23 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             c.base = cb;
             c.r = cr;
         }
-        const KernArgs kp = kernargs();
-        const int32_t pperiod = kp->part_period;
         c.part_me = 0;                                                    // made each step: not loop-carried
-        if (pperiod > 0) {                                                // S-11 partitions
-            const uint32_t ph = t % (uint32_t)pperiod;
-            if ((int64_t)ph < kp->part_len) {
-                if (k == 0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
-            } else {
-                c.part = 0;
+        if constexpr ((NET & NET_PART) != 0) {
+            const KernArgs kp = kernargs();
+            const int32_t pperiod = kp->part_period;
+            if (pperiod > 0) {                                            // S-11 partitions
+                const uint32_t ph = t % (uint32_t)pperiod;
+                if ((int64_t)ph < kp->part_len) {
+                    if (k == 0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
+                } else {
+                    c.part = 0;
+                }
+                c.part_me = lm((c.part >> c.r) & 1u);
             }
-            c.part_me = lm((c.part >> c.r) & 1u);
         }
         Counters cnt;
         cnt.clear();
-        Stepper<R, TB, RING>::step(p, c, n, cnt);
+        Stepper<R, TB, RING, NET>::step(p, c, n, cnt);
         c.clk.mark(PH_TDRAW);
         uint32_t v = 0;                                                     // lane cw <- wave total cw
 #pragma unroll
@@ -744,13 +748,29 @@ template <int R> struct InitL {
         init_kernel<R><<<nb, BLOCK, 0, e->stream>>>(e->dp);
     }
 };
+// The step kernel for the engine's network faults: at the replica counts of
+// BASELINE.json's configurations (3, 5, 7) a kernel built for drops only
+// (config 3) or for partitions only (config 5, and no faults at all: config
+// 2), so the other's checks are compiled out; otherwise, and for both at once,
+// the NET_ALL kernel, which decides them at run time.
+typedef void (*StepKernel)(DevParams, uint32_t, int);
+template <int R, bool TB, bool RING>
+static StepKernel step_fn(const DevParams& d, const raft_params& p) {
+    if constexpr (R == 3 || R == 5 || R == 7) {
+        const bool drops = d.drop_thr16 != 0, parts = p.partition_period > 0 && p.partition_len > 0;
+        if (drops && !parts) return step_kernel<R, TB, RING, NET_DROP>;
+        if (!drops) return step_kernel<R, TB, RING, NET_PART>;
+    }
+    return step_kernel<R, TB, RING, NET_ALL>;
+}
 template <int R> struct StepL {
     static void run(raft_engine* e, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st, int b0, int b1,
                     uint32_t* partials) {
         const size_t lds = (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4;
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
-        auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? (e->p.log_window ? step_kernel<R, true, true> : step_kernel<R, true, false>)
-                                                     : (e->p.log_window ? step_kernel<R, false, true> : step_kernel<R, false, false>);
+        auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK
+                         ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p) : step_fn<R, true, false>(e->dp, e->p))
+                         : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p) : step_fn<R, false, false>(e->dp, e->p));
         // the launch's own start / stop timestamps (ev0, ev1 nullable): no
         // marker packets around the dispatch
         DevParams d = e->dp;

@@ -234,6 +234,22 @@ __device__ __forceinline__ bool no_drops(const DevParams& p) {
     return thr == 0;
 }
 
+// The network faults a step kernel is built for (its NET template argument):
+// NET_DROP, seeded message drops (drop_ppm > 0); NET_PART, partitions
+// (partition_period > 0).  A kernel without one of them compiles its checks
+// out (per vote / tick round: the drop compares of both directions, or the
+// partition-side extract and compare); NET_ALL decides both at run time.
+// The host picks the kernel from the engine's raft_params (raft_engine.hip).
+constexpr int NET_DROP = 1, NET_PART = 2, NET_ALL = NET_DROP | NET_PART;
+// no drop can happen: compile-time in a kernel built without NET_DROP, and
+// at run time (drop_ppm == 0) in a NET_ALL kernel
+template <int NET>
+__device__ __forceinline__ bool drops_off(const DevParams& p) {
+    if constexpr (!(NET & NET_DROP)) return true;
+    else if constexpr (NET == NET_ALL) return no_drops(p);
+    else return false;
+}
+
 __device__ __forceinline__ u32x4 draw(const DevParams& p, uint32_t c0, uint32_t gid, uint32_t purpose, uint32_t sub) {
     return philox4x32_10(c0, gid, purpose, sub, p.key0, p.key1);
 }
@@ -592,13 +608,16 @@ struct Ctx {
 // made once per round for both directions.  (Skipping its compares in waves
 // with no isolation or partition measured slower: the branches cost more
 // SALU issue than the VALU they save.)
-template <int R>
+template <int R, int NET>
 __device__ __forceinline__ uint64_t lost_net(const Ctx<R>& c, int s) {
-    return lm(s == c.iso) | c.iso_me |                                          // iso = -1: nobody isolated
-           (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
+    const uint64_t iso = lm(s == c.iso) | c.iso_me;                             // iso = -1: nobody isolated
+    if constexpr (!(NET & NET_PART)) return iso;
+    else return iso | (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
 }
+template <int NET>
 __device__ __forceinline__ uint64_t lost(const DevParams& p, uint64_t net, uint64_t mself, uint32_t dw, int b) {
-    return ~mself & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
+    if constexpr (!(NET & NET_DROP)) return ~mself & net;
+    else return ~mself & (net | lm(((dw >> (16 * b)) & 0xFFFFu) < p.drop_thr16));
 }
 
 // 16-bit drop uniforms of sender s for this lane as destination d (S-9):
@@ -627,10 +646,10 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int first_job, int
     return c.jl[((c.base + first_job) << 2) + q];
 }
 
-template <int R, bool HAVE_JOB>
+template <int R, bool HAVE_JOB, int NET>
 __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, uint64_t act,
                                               int s, uint32_t prefetched, int s_job) {
-    if (no_drops(p)) return 0u;
+    if (drops_off<NET>(p)) return 0u;
     uint32_t w = 0;
     uint64_t need = act;
     if constexpr (HAVE_JOB) {
@@ -669,7 +688,7 @@ __device__ __forceinline__ uint32_t timer_word(const DevParams& p, const Ctx<R>&
 // so the reference-parity kernel carries none of it.
 // RING: the log is a log_window ring, so every reference access is checked
 // against the window (a flat log keeps every slot: no access can miss).
-template <int R, bool TB, bool RING>
+template <int R, bool TB, bool RING, int NET>
 struct Stepper {
     using L = Lanes<R>;
     static constexpr int MAJ = L::MAJ;
@@ -745,8 +764,8 @@ struct Stepper {
         const uint64_t mme = lm(c.r == s);
         const uint64_t run = mtk & lm(role_s != RAFT_FOLLOWER);
         uint32_t dw;
-        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
-        else dw = drop_word<R, L::TICK_JOB>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
+        if constexpr (STAGED) dw = drops_off<NET>(p) ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
+        else dw = drop_word<R, L::TICK_JOB, NET>(p, c, RAFT_RNG_APPEND_DROP, run, s, c.dwt, c.s_tick);
         const uint64_t cancel = mtk & ~run & mme;                         // :117 cancel() (S-10)
         if (RARE(cancel)) n.fl &= ib(cancel) ? ~FL_HB : ~0u;
         cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
@@ -810,10 +829,10 @@ struct Stepper {
         // both directions' losses resolved here: a lane mask of comparisons made
         // in an earlier basic block (before the handler's log store) would be
         // re-materialised through a VGPR
-        const uint64_t net = lost_net(c, s);
-        const uint64_t lreq = ok & lost(p, net, mme, dw, 0);              // :170-172
+        const uint64_t net = lost_net<R, NET>(c, s);
+        const uint64_t lreq = ok & lost<NET>(p, net, mme, dw, 0);         // :170-172
         const uint64_t act = ok & ~lreq;
-        const uint64_t lresp = act & lost(p, net, mme, dw, 1);
+        const uint64_t lresp = act & lost<NET>(p, net, mme, dw, 1);
         int32_t rterm;
         uint64_t succ, stored;
         // no lane of act throws: ok implies prev >= -1
@@ -997,7 +1016,7 @@ struct Stepper {
     // (job_drop_word(c, s, s)) instead of one direct pass each.  Called in
     // wave-uniform control flow.
     __device__ __forceinline__ static void stage_sender_chunks(const DevParams& p, Ctx<R>& c, uint32_t purpose) {
-        if (no_drops(p)) return;
+        if (drops_off<NET>(p)) return;
         const u32x4 w = kdraw(p, c.t, c.gid(), purpose, (uint32_t)c.r);
         *(uint4*)&c.jl[(c.base + c.r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
         asm volatile("" ::: "memory");
@@ -1021,17 +1040,17 @@ struct Stepper {
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
         const int32_t st = bcast(n.term, sl);
         uint32_t dw;
-        if constexpr (STAGED) dw = no_drops(p) ? 0u : job_drop_word(c, s, s);         // stage_sender_chunks
-        else dw = drop_word<R, L::VOTE_JOB>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
+        if constexpr (STAGED) dw = drops_off<NET>(p) ? 0u : job_drop_word(c, s, s);   // stage_sender_chunks
+        else dw = drop_word<R, L::VOTE_JOB, NET>(p, c, RAFT_RNG_VOTE_DROP, mvr, s, c.dwv, c.s_vote);
         const uint64_t mine = mvr & lm((ms >> r) & 1u);
         const uint64_t mme = lm(r == s);
-        const uint64_t net = lost_net(c, s);
-        const uint64_t lreq = mine & lost(p, net, mme, dw, 0);      // retry{} swallows, Commons.kt:41
+        const uint64_t net = lost_net<R, NET>(c, s);
+        const uint64_t lreq = mine & lost<NET>(p, net, mme, dw, 0); // retry{} swallows, Commons.kt:41
         const uint64_t act = mine & ~lreq;
         int32_t rterm;
         uint64_t granted;
         vote_handler<TB, RING>(n.rep(), act, r + 1, rt, s + 1, rli, rlt, gapw, hasl, fs, cnt, rterm, granted);
-        const uint64_t lresp = act & lost(p, net, mme, dw, 1);
+        const uint64_t lresp = act & lost<NET>(p, net, mme, dw, 1);
         const uint64_t delivered = act & ~lresp;
         cnt.add(lreq | lresp, RAFT_C_MSG_DROPPED);
         const uint64_t him = delivered & lm(rterm > st);

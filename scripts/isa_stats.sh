@@ -10,8 +10,11 @@ d, kn = sys.argv[1], sys.argv[2]
 s = open(f'{d}/raft_engine-hip-amdgcn-amd-amdhsa-gfx950.s').read().split('\n')
 cur = None; st = {}
 for i, l in enumerate(s):
-    m = re.match(r'^(_Z\S*' + kn + r'ILi(\d)E\S*):', l)
-    if m: cur = m.group(2) + ("r" if "Lb1EEE" in l or "Lb0ELb1E" in l else ""); st[cur] = collections.Counter(); continue
+    m = re.match(r'^(_Z\S*' + kn + r'ILi(\d)ELb(\d)ELb(\d)E(?:Li(\d)E)?\S*):', l)
+    if m:
+        cur = m.group(2) + ("t" if m.group(3) == "1" else "") + ("r" if m.group(4) == "1" else "") + \
+              (("/net" + m.group(5)) if m.group(5) else "")
+        st[cur] = collections.Counter(); continue
     if cur and '; -- End function' in l:
         blk = '\n'.join(s[i:i + 30])
         for k in ['codeLenInByte', 'NumVgprs', 'NumSgprs', 'ScratchSize', 'Occupancy']:
