@@ -45,16 +45,35 @@ NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
 MAX_STEPS_PER_LAUNCH = 512
 # bench.py's launch length for the step kernels built for 7 waves per SIMD
-# (reference mode, flat log, R <= 5; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
+# (reference mode, flat log, R <= 5 or R = 7 without drops; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
 # the longest that keeps 7 step workgroups per CU within the LDS (STEP_K_7WG,
 # 433 steps).  The other kernels run 6 workgroups per CU at any length and
 # take the longest launch.
 BENCH_STEPS_PER_LAUNCH = 400
 
 
-def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0) -> int:
-    """Default fused launch length of bench.py for a kernel variant."""
-    seven = mode == MODE_REFERENCE and log_window == 0 and R <= 5
+# The network faults a step kernel is built for (raft_step.h NET_*): the
+# engine runs a drops-only or partitions-only kernel at R = 3, 5, 7 (the
+# other fault's checks compiled out), else the NET_ALL kernel
+NET_DROP, NET_PART, NET_ALL = 1, 2, 3
+
+
+def step_net(R: int, drop_ppm: int = 0, partition_period: int = 0, partition_len: int = 0) -> int:
+    """The NET of the step kernel the engine launches (raft_engine.hip step_fn)."""
+    drops, parts = drop_ppm > 0, partition_period > 0 and partition_len > 0
+    if R in (3, 5, 7):
+        if drops and not parts:
+            return NET_DROP
+        if not drops:
+            return NET_PART
+    return NET_ALL
+
+
+def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0, net: int = NET_ALL) -> int:
+    """Default fused launch length of bench.py for a kernel variant: 400 for the
+    7-waves-per-SIMD kernels (reference mode, flat log, R <= 5, or R = 7 built
+    for partitions only), the longest launch for the others."""
+    seven = mode == MODE_REFERENCE and log_window == 0 and (R <= 5 or (R == 7 and net == NET_PART))
     return BENCH_STEPS_PER_LAUNCH if seven else MAX_STEPS_PER_LAUNCH
 MAX_AE_ENTRIES = 8           # include/raft_engine.h RAFT_MAX_AE_ENTRIES
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}

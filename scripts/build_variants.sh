@@ -3,7 +3,7 @@
 # (raft-kotlin_amd/lib/libraft_engine_<name>.so, selected with RAFT_ENGINE_LIB
 # by scripts/ab.sh / scripts/ab_session.sh).  The product sources carry no
 # experiment switches: a variant is the working tree's csrc plus
-#   name:-DFLAGS ...        compiler flags (e.g. "w6:-DRAFT_STEP_WAVES_PER_EU(R,TB,RING)=6")
+#   name:-DFLAGS ...        compiler flags (e.g. "w6:-DRAFT_STEP_WAVES_PER_EU(R,TB,RING,NET)=6")
 #   name:patch=P[+P2...]    patches from scripts/variants/P.patch (e.g. "replay:patch=commit_replay")
 #   name:rev=REV            the csrc of a git revision instead of the working tree
 # Specs may combine parts with ';' ("nc7:patch=no_counters;-DRAFT_STEP_BLOCK=256").

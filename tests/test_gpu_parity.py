@@ -313,14 +313,16 @@ FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_
 # log (log_window 0: every slot, 130 GB at log_cap 3064), step_kernel<5, false,
 # false> at 7 waves per SIMD, launched at K = 400 by default and K = 20 by the
 # driver's `--steps 20` command; the 256-slot ring is step_kernel<5, false,
-# true> (6 waves).  Config 5 is always flat; bench.py launches it at K = 500
-# (launch_length(10^4, 512)).
+# true> (6 waves).  Config 5 is always flat; bench.py launches it at K = 400
+# (the partitions-only R = 7 kernel at 7 waves per SIMD; K = 500 and 512 run
+# it at 6 workgroups per CU).
 # A fourth element is the launch sub-ranges (streams); default: the engine's
 # automatic choice (3, the bench's configuration).
 FULL_SIZE_CASES = [
     (3, 0, 1), (3, 0, 20), (3, 0, abi.BENCH_STEPS_PER_LAUNCH), (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 1),
     (3, 256, 1), (3, 256, abi.BENCH_STEPS_PER_LAUNCH), (3, 256, abi.MAX_STEPS_PER_LAUNCH),
-    (5, 0, 1), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH), (5, 0, 500, 1), (5, 0, 500, 4),
+    (5, 0, 1), (5, 0, abi.BENCH_STEPS_PER_LAUNCH), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH),
+    (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 1), (5, 0, 500, 4),
 ]
 
 
