@@ -45,7 +45,7 @@ NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
 MAX_STEPS_PER_LAUNCH = 512
 # bench.py's launch length for the step kernels built for 7 waves per SIMD
-# (reference mode, flat log, R <= 5 or R = 7 without drops; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
+# (R <= 5, or R = 7 without drops; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
 # the longest that keeps 7 step workgroups per CU within the LDS (STEP_K_7WG,
 # 433 steps).  The other kernels run 6 workgroups per CU at any length and
 # take the longest launch.
@@ -71,9 +71,9 @@ def step_net(R: int, drop_ppm: int = 0, partition_period: int = 0, partition_len
 
 def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0, net: int = NET_ALL) -> int:
     """Default fused launch length of bench.py for a kernel variant: 400 for the
-    7-waves-per-SIMD kernels (reference mode, flat log, R <= 5, or R = 7 built
-    for partitions only), the longest launch for the others."""
-    seven = mode == MODE_REFERENCE and log_window == 0 and (R <= 5 or (R == 7 and net == NET_PART))
+    7-waves-per-SIMD kernels (R <= 5, or R = 7 built for partitions only; either
+    protocol mode, flat log or ring), the longest launch for the others."""
+    seven = R <= 5 or (R == 7 and net == NET_PART)
     return BENCH_STEPS_PER_LAUNCH if seven else MAX_STEPS_PER_LAUNCH
 MAX_AE_ENTRIES = 8           # include/raft_engine.h RAFT_MAX_AE_ENTRIES
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}

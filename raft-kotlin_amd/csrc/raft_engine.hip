@@ -170,16 +170,17 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 // without costing occupancy; the launch's two barriers (zeroing, final copy)
 // sit outside the step loop.
 // Waves per SIMD the register allocation targets: 7 (72 VGPRs, 94 SGPRs)
-// where the kernel fits them (the reference-mode, flat-log kernels at R <= 5,
-// and at R = 7 without drop checks), else 6 (80 VGPRs, 106 SGPRs).  Seven
+// where the kernel fits them (every kernel at R <= 5, and at R = 7 without
+// drop checks), else 6 (80 VGPRs, 106 SGPRs).  Seven
 // workgroups per CU also need the LDS of a launch of at most STEP_K_7WG steps,
 // which bench.py's default launch length respects.
 // (round 3: also R = 7 built for partitions only, config 5's kernel, which
 // the dropped drop checks brought to 72 VGPRs with 12 B of spills: +4.3 %,
-// profiles/r3_w7)
+// profiles/r3_w7; and the textbook-mode flat kernels, 72 VGPRs with 12-20 B
+// of spills: +4.4 % on config 3, +4 % on config 5, profiles/r3_tb7; and the
+// ring kernels, 72 VGPRs with 16 B of spills at R = 5: +3.8 %, profiles/r3_all7)
 #ifndef RAFT_STEP_WAVES_PER_EU
-#define RAFT_STEP_WAVES_PER_EU(R, TB, RING, NET) \
-    ((!(TB) && !(RING) && ((R) <= 5 || ((R) == 7 && (NET) == NET_PART))) ? 7 : 6)
+#define RAFT_STEP_WAVES_PER_EU(R, TB, RING, NET) (((R) <= 5 || ((R) == 7 && (NET) == NET_PART)) ? 7 : 6)
 #endif
 // NET: the network faults the kernel is built for (raft_step.h NET_DROP /
 // NET_PART; the host's step_fn picks it from raft_params).

@@ -89,7 +89,7 @@ def test_cpu_share_is_positive():
 
 
 def test_default_launch_length_per_kernel_variant():
-    """7-waves-per-SIMD kernels (reference mode, flat log, R <= 5) launch at most
+    """7-waves-per-SIMD kernels (R <= 5, or R = 7 without drops) launch at most
     abi.BENCH_STEPS_PER_LAUNCH steps so 7 workgroups fit a CU's LDS; the others
     take the longest launch (raft_engine.hip RAFT_STEP_WAVES_PER_EU)."""
     assert abi.bench_steps_per_launch(5) == abi.BENCH_STEPS_PER_LAUNCH == 400
@@ -101,8 +101,8 @@ def test_default_launch_length_per_kernel_variant():
     assert abi.step_net(5, drop_ppm=abi.CONFIGS[3]["drop_ppm"]) == abi.NET_DROP
     assert abi.step_net(5, drop_ppm=1, partition_period=50, partition_len=25) == abi.NET_ALL
     assert abi.step_net(4, drop_ppm=1) == abi.NET_ALL and abi.step_net(3) == abi.NET_PART
-    assert abi.bench_steps_per_launch(5, abi.MODE_TEXTBOOK) == abi.MAX_STEPS_PER_LAUNCH
-    assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 256) == abi.MAX_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(5, abi.MODE_TEXTBOOK) == abi.BENCH_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 256) == abi.BENCH_STEPS_PER_LAUNCH
     assert bench.launch_length(10_000, 400) == 400 and bench.launch_length(20, 400) == 20
 
 

@@ -313,7 +313,7 @@ FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_
 # log (log_window 0: every slot, 130 GB at log_cap 3064), step_kernel<5, false,
 # false> at 7 waves per SIMD, launched at K = 400 by default and K = 20 by the
 # driver's `--steps 20` command; the 256-slot ring is step_kernel<5, false,
-# true> (6 waves).  Config 5 is always flat; bench.py launches it at K = 400
+# true> (7 waves as well).  Config 5 is always flat; bench.py launches it at K = 400
 # (the partitions-only R = 7 kernel at 7 waves per SIMD; K = 500 and 512 run
 # it at 6 workgroups per CU).
 # A fourth element is the launch sub-ranges (streams); default: the engine's
