@@ -153,6 +153,24 @@ def test_other_replica_counts(R):
     run_lockstep(e, o, 400, 50, f"R={R}")
 
 
+@pytest.mark.parametrize("R,faults", [(3, "drops"), (5, "drops"), (7, "drops"), (3, "partitions"),
+                                      (5, "partitions"), (7, "partitions"), (5, "none")])
+def test_network_fault_kernels(R, faults):
+    """The step kernels built for one network fault (raft_step.h NET_DROP /
+    NET_PART: the engine picks them at R = 3, 5, 7 from raft_params), each
+    against the oracle: drops without partitions, partitions without drops,
+    and neither (the partitions-only kernel with no partition configured)."""
+    kw = dict(R=R, G=3000, seed=200 + R, log_cap=300, churn_ppm=20_000, churn_steps=15, cmd_ppm=500_000)
+    if faults == "drops":
+        kw.update(drop_ppm=100_000)
+    elif faults == "partitions":
+        kw.update(partition_period=40, partition_len=10)
+    want = {"drops": abi.NET_DROP, "partitions": abi.NET_PART, "none": abi.NET_PART}[faults]
+    assert abi.step_net(R, kw.get("drop_ppm", 0), kw.get("partition_period", 0), kw.get("partition_len", 0)) == want
+    e, o = pair(**kw)
+    run_lockstep(e, o, 400, 50, f"R={R} {faults}")
+
+
 def test_steps_per_launch_invariance():
     kw = dict(abi.CONFIGS[3])
     kw.update(G=5000, churn_ppm=10_000)
