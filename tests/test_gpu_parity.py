@@ -171,6 +171,20 @@ def test_network_fault_kernels(R, faults):
     run_lockstep(e, o, 400, 50, f"R={R} {faults}")
 
 
+@pytest.mark.parametrize("mode", [abi.MODE_REFERENCE, abi.MODE_TEXTBOOK])
+def test_log_overflow_on_engine(mode):
+    """S-12 on the GPU: a log_cap too small for the run.  Appends beyond it
+    are refused and counted (RAFT_C_LOG_OVERFLOW) in the same steps as the
+    oracle counts them (tests/test_oracle_kats.py pins the oracle's rule), and
+    the state and logs stay equal."""
+    kw = dict(abi.CONFIGS[3], G=4000, churn_ppm=20_000, cmd_ppm=1_000_000, log_cap=40, mode=mode)
+    e, o = pair(**kw)
+    run_lockstep(e, o, 300, 50, f"overflow mode={mode}")
+    e2 = RaftEngine(abi.make_params(**kw))
+    c = e2.step(300)
+    assert c[:, abi.C_INDEX["log_overflow"]].sum() > 0, "the run must overflow its log_cap"
+
+
 def test_steps_per_launch_invariance():
     kw = dict(abi.CONFIGS[3])
     kw.update(G=5000, churn_ppm=10_000)
