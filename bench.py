@@ -566,9 +566,8 @@ def strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk,
            "ms_per_step": leg["elapsed"] * 1e3 / args.steps, "groups_total": args.groups, "groups_per_rank": per_rank,
            "steps_per_launch": L, "subranges": nsub, "log_window": window,
            "step_waves_per_rank": -(-G // (64 // R)),
-           "grid_fill": grid_fill(G, R, L, abi.bench_steps_per_launch(R, mode, window, abi.step_net(
-               R, kw.get("drop_ppm", 0), kw.get("partition_period", 0), kw.get("partition_len", 0)))
-               < abi.MAX_STEPS_PER_LAUNCH),
+           "grid_fill": grid_fill(G, R, L, abi.bench_steps_per_launch(R, mode, window, abi.step_net_of(kw))
+                                < abi.MAX_STEPS_PER_LAUNCH),
            "kernel_avg_ms_per_rank": leg["kern_avg_per_rank"],
            "timing": {"wall_ms": leg["wall"] * 1e3, "stream_event_ms": leg["ev_ms"],
                       "step_kernel_ms_total": leg["kern_ms"]},
@@ -662,7 +661,7 @@ def main(argv=None, result=None):
         window = 0 if args.config == 5 or flat <= 0.6 * hbm else 256
     log_cap = max(log_cap, window)                          # the window never exceeds the physLen limit
     mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
-    net = abi.step_net(R, kw.get("drop_ppm", 0), kw.get("partition_period", 0), kw.get("partition_len", 0))
+    net = abi.step_net_of(kw)
     spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window, net)
     L = launch_length(args.steps, spl)                      # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce

@@ -52,21 +52,32 @@ MAX_STEPS_PER_LAUNCH = 512
 BENCH_STEPS_PER_LAUNCH = 400
 
 
-# The network faults a step kernel is built for (raft_step.h NET_*): the
-# engine runs a drops-only or partitions-only kernel at R = 3, 5, 7 (the
-# other fault's checks compiled out), else the NET_ALL kernel
-NET_DROP, NET_PART, NET_ALL = 1, 2, 3
+# The network faults a step kernel is built for (raft_step.h NET_*): at
+# R = 3, 5, 7 the engine runs a kernel for drops + isolation churn without
+# partitions (config 3) or for partitions alone (configs 5 and 2), the other
+# checks compiled out; else the NET_ALL kernel
+NET_DROP, NET_PART, NET_ISO = 1, 2, 4
+NET_ALL = NET_DROP | NET_PART | NET_ISO
 
 
-def step_net(R: int, drop_ppm: int = 0, partition_period: int = 0, partition_len: int = 0) -> int:
-    """The NET of the step kernel the engine launches (raft_engine.hip step_fn)."""
+def step_net(R: int, drop_ppm: int = 0, partition_period: int = 0, partition_len: int = 0,
+             churn_ppm: int = 0, iso_written: bool = False) -> int:
+    """The NET of the step kernel the engine launches (raft_engine.hip step_fn);
+    iso_written: an isolation word was written into the state."""
     drops, parts = drop_ppm > 0, partition_period > 0 and partition_len > 0
+    iso = churn_ppm > 0 or iso_written
     if R in (3, 5, 7):
         if drops and not parts:
-            return NET_DROP
-        if not drops:
+            return NET_DROP | NET_ISO
+        if not drops and not iso:
             return NET_PART
     return NET_ALL
+
+
+def step_net_of(kw: dict) -> int:
+    """step_net of a raft_params keyword dict (abi.CONFIGS entries)."""
+    return step_net(kw["R"], kw.get("drop_ppm", 0), kw.get("partition_period", 0), kw.get("partition_len", 0),
+                    kw.get("churn_ppm", 0))
 
 
 def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0, net: int = NET_ALL) -> int:

@@ -726,6 +726,7 @@ struct raft_engine {
     unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
     // step-kernel event timing
     bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
+    bool iso_written;           // write_state stored a nonzero isolation word (step_fn: NET_ISO kernels)
     bool timing;
     std::vector<hipEvent_t> ev;  // pool, pairs (one per sub-range launch)
     size_t ev_used;
@@ -754,17 +755,18 @@ template <int R> struct InitL {
     }
 };
 // The step kernel for the engine's network faults: at the replica counts of
-// BASELINE.json's configurations (3, 5, 7) a kernel built for drops only
-// (config 3) or for partitions only (config 5, and no faults at all: config
-// 2), so the other's checks are compiled out; otherwise, and for both at once,
-// the NET_ALL kernel, which decides them at run time.
+// BASELINE.json's configurations (3, 5, 7) a kernel built for drops and
+// isolation churn without partitions (config 3), or for partitions alone
+// (config 5, and no faults at all: config 2), so the other checks are
+// compiled out; otherwise the NET_ALL kernel.  `iso`: churn is configured or
+// an isolation word was written into the state (raft_engine_write_state).
 typedef void (*StepKernel)(DevParams, uint32_t, int);
 template <int R, bool TB, bool RING>
-static StepKernel step_fn(const DevParams& d, const raft_params& p) {
+static StepKernel step_fn(const DevParams& d, const raft_params& p, bool iso) {
     if constexpr (R == 3 || R == 5 || R == 7) {
         const bool drops = d.drop_thr16 != 0, parts = p.partition_period > 0 && p.partition_len > 0;
-        if (drops && !parts) return step_kernel<R, TB, RING, NET_DROP>;
-        if (!drops) return step_kernel<R, TB, RING, NET_PART>;
+        if (drops && !parts) return step_kernel<R, TB, RING, NET_DROP | NET_ISO>;
+        if (!drops && !iso) return step_kernel<R, TB, RING, NET_PART>;
     }
     return step_kernel<R, TB, RING, NET_ALL>;
 }
@@ -773,9 +775,12 @@ template <int R> struct StepL {
                     uint32_t* partials) {
         const size_t lds = (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4;
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
+        const bool iso = e->dp.churn_thr32 != 0 || e->iso_written;
         auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK
-                         ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p) : step_fn<R, true, false>(e->dp, e->p))
-                         : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p) : step_fn<R, false, false>(e->dp, e->p));
+                         ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p, iso)
+                                            : step_fn<R, true, false>(e->dp, e->p, iso))
+                         : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p, iso)
+                                            : step_fn<R, false, false>(e->dp, e->p, iso));
         // the launch's own start / stop timestamps (ev0, ev1 nullable): no
         // marker packets around the dispatch
         DevParams d = e->dp;
@@ -1249,6 +1254,8 @@ int raft_engine_write_state(raft_engine* e, int64_t g0, int64_t n, const int32_t
             if (f[RAFT_F_LAST] < 0 || f[RAFT_F_LAST] > f[RAFT_F_PHYS] || f[RAFT_F_PHYS] > e->p.log_cap)
                 return fail(RAFT_EINVAL, "state violates 0 <= lastIndex <= physLen <= log_cap");
         }
+    for (int64_t j = 0; j < n; ++j)              // an isolation word: only kernels with NET_ISO from now on
+        if (in[j * W + W - 2] != 0) e->iso_written = true;
     HIP_TRY(hipSetDevice(e->device));
     e->fork_needed = true;
     const size_t bytes = (size_t)n * W * 4;

@@ -236,11 +236,14 @@ __device__ __forceinline__ bool no_drops(const DevParams& p) {
 
 // The network faults a step kernel is built for (its NET template argument):
 // NET_DROP, seeded message drops (drop_ppm > 0); NET_PART, partitions
-// (partition_period > 0).  A kernel without one of them compiles its checks
-// out (per vote / tick round: the drop compares of both directions, or the
-// partition-side extract and compare); NET_ALL decides both at run time.
-// The host picks the kernel from the engine's raft_params (raft_engine.hip).
-constexpr int NET_DROP = 1, NET_PART = 2, NET_ALL = NET_DROP | NET_PART;
+// (partition_period > 0); NET_ISO, leader isolation (churn_ppm > 0, or an
+// isolation word written into the state).  A kernel without one of them
+// compiles its checks out (per vote / tick round: the drop compares of both
+// directions, the partition-side extract and compare, or the isolated-sender
+// compare; per step: H's isolation bookkeeping); NET_ALL decides drops at run
+// time.  The host picks the kernel from the engine's raft_params
+// (raft_engine.hip step_fn).
+constexpr int NET_DROP = 1, NET_PART = 2, NET_ISO = 4, NET_ALL = NET_DROP | NET_PART | NET_ISO;
 // no drop can happen: compile-time in a kernel built without NET_DROP, and
 // at run time (drop_ppm == 0) in a NET_ALL kernel
 template <int NET>
@@ -610,9 +613,11 @@ struct Ctx {
 // SALU issue than the VALU they save.)
 template <int R, int NET>
 __device__ __forceinline__ uint64_t lost_net(const Ctx<R>& c, int s) {
-    const uint64_t iso = lm(s == c.iso) | c.iso_me;                             // iso = -1: nobody isolated
-    if constexpr (!(NET & NET_PART)) return iso;
-    else return iso | (c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u)));   // s, d on two sides
+    uint64_t net = 0;
+    if constexpr ((NET & NET_ISO) != 0) net = lm(s == c.iso) | c.iso_me;        // iso = -1: nobody isolated
+    if constexpr ((NET & NET_PART) != 0)
+        net |= c.part_me ^ lm(__builtin_amdgcn_ubfe(c.part, (uint32_t)s, 1u));    // s, d on two sides
+    return net;
 }
 template <int NET>
 __device__ __forceinline__ uint64_t lost(const DevParams& p, uint64_t net, uint64_t mself, uint32_t dw, int b) {
@@ -1232,7 +1237,8 @@ struct Stepper {
             c.iso = -1;
             c.iso_me = 0;
             // only waves where an isolation runs or may start (~1/5) do the rest
-            if (RARE(lm(n.iso != 0) | lm((uint64_t)hw0 < churn_thr))) {
+            // (none in a kernel built without NET_ISO: no churn, no isolation word)
+            if ((NET & NET_ISO) != 0 && RARE(lm(n.iso != 0) | lm((uint64_t)hw0 < churn_thr))) {
                 const int32_t churn_steps = kp->churn_steps;
                 int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
                 if (rem > 0) { rem--; if (rem == 0) rep = 0; }

@@ -96,10 +96,13 @@ def test_default_launch_length_per_kernel_variant():
     assert abi.bench_steps_per_launch(3) == 400
     assert abi.bench_steps_per_launch(7) == abi.MAX_STEPS_PER_LAUNCH
     # config 5 (R = 7, partitions, no drops) runs the 7-wave partitions-only kernel
-    net5 = abi.step_net(**{k: abi.CONFIGS[5][k] for k in ("R", "partition_period", "partition_len")})
+    net5 = abi.step_net_of(abi.CONFIGS[5])
     assert net5 == abi.NET_PART and abi.bench_steps_per_launch(7, abi.MODE_REFERENCE, 0, net5) == 400
-    assert abi.step_net(5, drop_ppm=abi.CONFIGS[3]["drop_ppm"]) == abi.NET_DROP
+    assert abi.step_net_of(abi.CONFIGS[3]) == abi.NET_DROP | abi.NET_ISO
+    assert abi.step_net_of(abi.CONFIGS[2]) == abi.NET_PART
     assert abi.step_net(5, drop_ppm=1, partition_period=50, partition_len=25) == abi.NET_ALL
+    assert abi.step_net(7, partition_period=50, partition_len=25, churn_ppm=1) == abi.NET_ALL
+    assert abi.step_net(7, iso_written=True) == abi.NET_ALL
     assert abi.step_net(4, drop_ppm=1) == abi.NET_ALL and abi.step_net(3) == abi.NET_PART
     assert abi.bench_steps_per_launch(5, abi.MODE_TEXTBOOK) == abi.BENCH_STEPS_PER_LAUNCH
     assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 256) == abi.BENCH_STEPS_PER_LAUNCH

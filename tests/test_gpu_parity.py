@@ -153,20 +153,28 @@ def test_other_replica_counts(R):
     run_lockstep(e, o, 400, 50, f"R={R}")
 
 
-@pytest.mark.parametrize("R,faults", [(3, "drops"), (5, "drops"), (7, "drops"), (3, "partitions"),
-                                      (5, "partitions"), (7, "partitions"), (5, "none")])
+NET_CASES = [(3, "drops+churn"), (5, "drops+churn"), (7, "drops+churn"), (5, "drops"), (3, "partitions"),
+             (5, "partitions"), (7, "partitions"), (7, "partitions+churn"), (5, "none"), (5, "churn")]
+
+
+@pytest.mark.parametrize("R,faults", NET_CASES, ids=[f"{r}-{f}" for r, f in NET_CASES])
 def test_network_fault_kernels(R, faults):
-    """The step kernels built for one network fault (raft_step.h NET_DROP /
-    NET_PART: the engine picks them at R = 3, 5, 7 from raft_params), each
-    against the oracle: drops without partitions, partitions without drops,
-    and neither (the partitions-only kernel with no partition configured)."""
-    kw = dict(R=R, G=3000, seed=200 + R, log_cap=300, churn_ppm=20_000, churn_steps=15, cmd_ppm=500_000)
-    if faults == "drops":
+    """The step kernels built for the workload's network faults (raft_step.h
+    NET_*: the engine picks them at R = 3, 5, 7 from raft_params), each
+    against the oracle: drops (with and without isolation churn) on the
+    drops + isolation kernel, partitions alone and no faults at all on the
+    partitions-only kernel, and the mixes that need the NET_ALL kernel."""
+    kw = dict(R=R, G=3000, seed=200 + R, log_cap=300, cmd_ppm=500_000)
+    if "churn" in faults:
+        kw.update(churn_ppm=20_000, churn_steps=15)
+    if "drops" in faults:
         kw.update(drop_ppm=100_000)
-    elif faults == "partitions":
+    if "partitions" in faults:
         kw.update(partition_period=40, partition_len=10)
-    want = {"drops": abi.NET_DROP, "partitions": abi.NET_PART, "none": abi.NET_PART}[faults]
-    assert abi.step_net(R, kw.get("drop_ppm", 0), kw.get("partition_period", 0), kw.get("partition_len", 0)) == want
+    want = {"drops+churn": abi.NET_DROP | abi.NET_ISO, "drops": abi.NET_DROP | abi.NET_ISO,
+            "partitions": abi.NET_PART, "none": abi.NET_PART, "partitions+churn": abi.NET_ALL,
+            "churn": abi.NET_ALL}[faults]
+    assert abi.step_net_of(kw) == want
     e, o = pair(**kw)
     run_lockstep(e, o, 400, 50, f"R={R} {faults}")
 
