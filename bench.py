@@ -364,7 +364,8 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
     """The drop-in service path (RaftServer.vote() / append(), RaftServer.kt:228-287):
     raft_vote_batch_dev / raft_append_batch_dev on n random messages already
     in HBM (key, stable radix sort, one lane per replica run), and the same
-    through the host entry points (pinned staging and PCIe both ways).  The
+    through the host entry points (from pageable arrays through pinned
+    staging, and from page-locked arrays by direct DMA).  The
     first device batch of each kind is checked against the oracle's handlers
     on a sample of groups: each sampled group's state and log are copied into
     its own oracle, which applies the batch's messages to that group in batch
@@ -434,16 +435,29 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         for _ in range(reps_h):
             hfn(group, dst, hreq)
         dt_host = time.perf_counter() - t0
+        # timed: page-locked host buffers (the engine's DMA reads and writes
+        # the caller's arrays directly, no staging copy)
+        pin = [torch.from_numpy(np.ascontiguousarray(a)).pin_memory() for a in (group, dst, req)]
+        pout = torch.zeros((n, resp_w), dtype=torch.int32).pin_memory()
+        pg, pd, pq, po = pin[0].numpy(), pin[1].numpy(), pin[2].numpy(), pout.numpy()
+        hfn(pg, pd, pq, out=po)
+        t0 = time.perf_counter()
+        for _ in range(args.handler_reps):
+            hfn(pg, pd, pq, out=po)
+        dt_pin = time.perf_counter() - t0
         out[kind] = {"messages_per_s_device": n * args.handler_reps / dt_dev,
                      "ms_per_batch_device": dt_dev * 1e3 / args.handler_reps,
                      "messages_per_s_host_buffers": n * reps_h / dt_host,
                      "ms_per_batch_host_buffers": dt_host * 1e3 / reps_h,
+                     "messages_per_s_pinned_host": n * args.handler_reps / dt_pin,
+                     "ms_per_batch_pinned_host": dt_pin * 1e3 / args.handler_reps,
                      "parity_sample_groups": int(sample.size), "parity_sample_messages": int(sel.sum()),
                      "parity_mismatches": int(bad)}
     out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a key kernel, a stable hipcub radix sort "
                    "over the key bits, the handler kernel (one lane per replica run, messages in batch order) and "
-                   "one status synchronisation; _host_buffers: the same through the host entry points (engine-owned "
-                   "pinned staging, PCIe both ways). The engine holds the bench run's final state; the messages are "
+                   "one status synchronisation; _host_buffers: the same through the host entry points from pageable "
+                   "arrays (multi-threaded copy into engine-owned pinned staging, PCIe both ways); _pinned_host: from "
+                   "page-locked arrays, which the DMA reads and writes directly. The engine holds the bench run's final state; the messages are "
                    "random (bench.handler_requests). Parity: the first batch of each kind against the oracle's "
                    "handlers on the sampled groups")
     return out

@@ -184,27 +184,39 @@ class RaftEngine:
             raise ValueError(f"{what}: group {g.shape} and replica {d.shape} must be 1-D with {n} entries")
         return g, d
 
-    def vote_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
+    @staticmethod
+    def _batch_out(out, n: int, w: int, what: str) -> np.ndarray:
+        """The response array: a new [n, w] int32 array, or the caller's (e.g. a
+        view of page-locked memory, which the engine's DMA writes directly)."""
+        if out is None:
+            return np.zeros((n, w), dtype=np.int32)
+        if out.dtype != np.int32 or out.shape != (n, w) or not out.flags.c_contiguous:
+            raise ValueError(f"{what}: out must be a C-contiguous int32 array of shape {(n, w)}")
+        return out
+
+    def vote_batch(self, group, dst, req: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
         """req: [n, 4] int32 (term, candidateId, lastLogIndex, lastLogTerm) ->
-        [n, 2] int32 (term, voteGranted)."""
+        [n, 2] int32 (term, voteGranted), into `out` when given.  Page-locked
+        arrays (all four) are moved by DMA with no staging copy."""
         q = np.ascontiguousarray(req, dtype=np.int32).reshape(-1, 4)
         g, d = self._batch_index(group, dst, q.shape[0], "vote_batch")
-        out = np.zeros((q.shape[0], 2), dtype=np.int32)
+        out = self._batch_out(out, q.shape[0], 2, "vote_batch")
         self._check(self._lib.raft_vote_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
                                               abi.ptr(q, abi.raft_vote_req), abi.ptr(out, abi.raft_vote_resp),
                                               q.shape[0]), "raft_vote_batch")
         return out
 
-    def append_batch(self, group, dst, req: np.ndarray) -> np.ndarray:
+    def append_batch(self, group, dst, req: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
         """req: [n, 8] int32 (term, leaderId, prevLogIndex, prevLogTerm, hasEntry,
-        entryTerm, entryCmd(u32 bits), leaderCommit) -> [n, 3] (term, success, status)."""
+        entryTerm, entryCmd(u32 bits), leaderCommit) -> [n, 3] (term, success, status),
+        into `out` when given."""
         req = np.asarray(req)
         if req.dtype == np.int32 or req.dtype == np.uint32:       # already the struct's 32-bit words
             q = np.ascontiguousarray(req).view(np.int32).reshape(-1, 8)
         else:
             q = np.ascontiguousarray(req).astype(np.int64).astype(np.uint32).view(np.int32).reshape(-1, 8)
         g, d = self._batch_index(group, dst, q.shape[0], "append_batch")
-        out = np.zeros((q.shape[0], 3), dtype=np.int32)
+        out = self._batch_out(out, q.shape[0], 3, "append_batch")
         self._check(self._lib.raft_append_batch(self._h, abi.ptr(g, C.c_int64), abi.ptr(d, C.c_int32),
                                                 abi.ptr(q, abi.raft_append_req), abi.ptr(out, abi.raft_append_resp),
                                                 q.shape[0]), "raft_append_batch")

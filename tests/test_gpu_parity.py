@@ -508,6 +508,43 @@ def test_handler_batches_vs_oracle(mode, G, n):
     assert_same_logs(se, e.read_log(), o.read_log(), R, "handlers")
 
 
+def test_pinned_host_batches_match_pageable():
+    """Page-locked host arrays take the direct-DMA path of raft_*_batch (no
+    staging copy), pageable ones the threaded copy into the engine's pinned
+    staging: both leave the same responses, state and logs, at a batch large
+    enough for the threaded copy (> 4 MB of requests)."""
+    import torch
+    rng = np.random.default_rng(12)
+    R, G, cap, n = 5, 2000, 8, 300_000
+    w, lt, lc = random_states(rng, G, R, cap)
+    a, b = (RaftEngine(abi.make_params(R=R, G=G, log_cap=cap, seed=4)) for _ in range(2))
+    for x in (a, b):
+        x.write_state(w)
+        x.write_log(lt, lc)
+    grp = rng.integers(0, G, size=n).astype(np.int64)
+    dst = rng.integers(0, R, size=n).astype(np.int32)
+    vq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(0, cap + 1, n),
+                   rng.integers(0, 4, n)], axis=1).astype(np.int32)
+    aq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(-1, cap, n),
+                   rng.integers(-1, 4, n), rng.integers(0, 2, n), rng.integers(0, 6, n),
+                   rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)],
+                  axis=1).astype(np.int64).astype(np.uint32).view(np.int32)
+    pin = lambda x: torch.from_numpy(np.ascontiguousarray(x)).pin_memory().numpy()   # noqa: E731
+    pg, pd = pin(grp), pin(dst)
+    ve = a.vote_batch(grp, dst, vq)
+    pv = pin(np.zeros((n, 2), np.int32))
+    assert b.vote_batch(pg, pd, pin(vq), out=pv) is pv
+    assert np.array_equal(ve, pv)
+    ae = a.append_batch(grp, dst, aq)
+    pa = pin(np.zeros((n, 3), np.int32))
+    b.append_batch(pg, pd, pin(aq), out=pa)
+    assert np.array_equal(ae, pa)
+    sa = a.read_state()
+    assert np.array_equal(sa, b.read_state())
+    assert_same_logs(sa, a.read_log(), b.read_log(), R, "pinned vs pageable batches")
+    assert a.digest() == b.digest()
+
+
 def test_device_batches_match_host_batches():
     """raft_*_batch_dev on HBM-resident messages (torch tensors) leave the
     same responses, state and logs as the host entry points on an identical
