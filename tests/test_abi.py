@@ -125,3 +125,11 @@ def test_missing_entry_points_bind_stubs(monkeypatch):
         lib = abi.load_library(other)
     with pytest.raises(RuntimeError, match="not in this engine build"):
         lib.raft_engine_subranges(None)
+
+
+def test_host_alloc_arguments(lib):
+    """raft_host_alloc refuses a non-positive size with a message; freeing NULL
+    is a no-op (the page-locked allocation itself needs the HIP runtime: GPU test)."""
+    assert lib.raft_host_alloc(0) is None
+    assert b"positive" in lib.raft_last_error()
+    assert lib.raft_host_free(None) == abi.RAFT_OK

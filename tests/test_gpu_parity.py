@@ -6,6 +6,7 @@ oracle finishes in seconds; the full-size configuration is checked on a random
 sample of groups (the oracle can run any subset of global group ids, since
 groups are independent and all randomness is keyed by the global id).
 """
+import ctypes as C
 import importlib
 import os
 
@@ -530,7 +531,13 @@ def test_pinned_host_batches_match_pageable():
                    rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)],
                   axis=1).astype(np.int64).astype(np.uint32).view(np.int32)
     pin = lambda x: torch.from_numpy(np.ascontiguousarray(x)).pin_memory().numpy()   # noqa: E731
-    pg, pd = pin(grp), pin(dst)
+    pg = pin(grp)
+    # the replica indices in the engine's own page-locked allocation (raft_host_alloc)
+    lib = abi.load_library()
+    raw = lib.raft_host_alloc(n * 4)
+    assert raw, lib.raft_last_error()
+    pd = np.ctypeslib.as_array((C.c_int32 * n).from_address(raw))
+    pd[:] = dst
     ve = a.vote_batch(grp, dst, vq)
     pv = pin(np.zeros((n, 2), np.int32))
     assert b.vote_batch(pg, pd, pin(vq), out=pv) is pv
@@ -543,6 +550,8 @@ def test_pinned_host_batches_match_pageable():
     assert np.array_equal(sa, b.read_state())
     assert_same_logs(sa, a.read_log(), b.read_log(), R, "pinned vs pageable batches")
     assert a.digest() == b.digest()
+    del pd
+    assert lib.raft_host_free(raw) == abi.RAFT_OK
 
 
 def test_device_batches_match_host_batches():
