@@ -11,7 +11,8 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 SRC = os.path.join(PKG, "csrc", "raft_engine.hip")
-SRCS = [SRC, os.path.join(PKG, "csrc", "raft_wire.cpp")]          # the wire codec is host code
+SRCS = [SRC, os.path.join(PKG, "csrc", "raft_wire.cpp"),           # the wire codec is host code
+        os.path.join(PKG, "csrc", "raft_host.cpp")]                  # page-locked batch memory
 HDRS = [os.path.join(PKG, "csrc", h) for h in ("raft_step.h", "philox.h")] + [
     os.path.join(ROOT, "include", h) for h in ("raft_engine.h", "raft_wire.h")]
 OUT = os.path.join(PKG, "lib", "libraft_engine.so")

@@ -1481,26 +1481,6 @@ static int run_batch(raft_engine* e, int kind, const int64_t* group, const int32
     return rc;
 }
 
-void* raft_host_alloc(int64_t bytes) {
-    if (bytes <= 0) {
-        fail(RAFT_EINVAL, "raft_host_alloc: bytes must be positive");
-        return nullptr;
-    }
-    void* p = nullptr;
-    const hipError_t err = hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault);
-    if (err != hipSuccess) {
-        fail(RAFT_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(err));
-        return nullptr;
-    }
-    return p;
-}
-
-int raft_host_free(void* p) {
-    if (!p) return RAFT_OK;
-    HIP_TRY(hipHostFree(p));
-    return RAFT_OK;
-}
-
 static int run_batch_on_device(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
                                size_t resp_sz, void* resp, int64_t n) {
     if (int rc = check_batch_args(e, n, group, dst, req, resp_sz, resp)) return rc;
