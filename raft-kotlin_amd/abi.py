@@ -52,23 +52,25 @@ MAX_STEPS_PER_LAUNCH = 512
 BENCH_STEPS_PER_LAUNCH = 400
 
 
-# The network faults a step kernel is built for (raft_step.h NET_*): at
-# R = 3, 5, 7 the engine runs a kernel for drops + isolation churn without
-# partitions (config 3) or for partitions alone (configs 5 and 2), the other
+# The network faults (and command harness) a step kernel is built for
+# (raft_step.h NET_*): at R = 3, 5, 7 the engine runs a kernel for drops +
+# isolation churn without partitions with config 3's command harness (lowest
+# LEADER, no limit), or for partitions alone (configs 5, 2, 1), the other
 # checks compiled out; else the NET_ALL kernel
-NET_DROP, NET_PART, NET_ISO = 1, 2, 4
+NET_DROP, NET_PART, NET_ISO, NET_CMDLOW = 1, 2, 4, 8
 NET_ALL = NET_DROP | NET_PART | NET_ISO
 
 
 def step_net(R: int, drop_ppm: int = 0, partition_period: int = 0, partition_len: int = 0,
-             churn_ppm: int = 0, iso_written: bool = False) -> int:
+             churn_ppm: int = 0, iso_written: bool = False, cmd_mode: int = 0, cmd_limit: int = 0) -> int:
     """The NET of the step kernel the engine launches (raft_engine.hip step_fn);
     iso_written: an isolation word was written into the state."""
     drops, parts = drop_ppm > 0, partition_period > 0 and partition_len > 0
     iso = churn_ppm > 0 or iso_written
+    cmdlow = cmd_mode == CMD_LOWEST_LEADER and cmd_limit == 0
     if R in (3, 5, 7):
-        if drops and not parts:
-            return NET_DROP | NET_ISO
+        if drops and not parts and cmdlow:
+            return NET_DROP | NET_ISO | NET_CMDLOW
         if not drops and not iso:
             return NET_PART
     return NET_ALL
@@ -77,7 +79,8 @@ def step_net(R: int, drop_ppm: int = 0, partition_period: int = 0, partition_len
 def step_net_of(kw: dict) -> int:
     """step_net of a raft_params keyword dict (abi.CONFIGS entries)."""
     return step_net(kw["R"], kw.get("drop_ppm", 0), kw.get("partition_period", 0), kw.get("partition_len", 0),
-                    kw.get("churn_ppm", 0))
+                    kw.get("churn_ppm", 0), cmd_mode=kw.get("cmd_mode", CMD_LOWEST_LEADER),
+                    cmd_limit=kw.get("cmd_limit", 0))
 
 
 def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0, net: int = NET_ALL) -> int:

@@ -757,16 +757,18 @@ template <int R> struct InitL {
 };
 // The step kernel for the engine's network faults: at the replica counts of
 // BASELINE.json's configurations (3, 5, 7) a kernel built for drops and
-// isolation churn without partitions (config 3), or for partitions alone
-// (config 5, and no faults at all: config 2), so the other checks are
-// compiled out; otherwise the NET_ALL kernel.  `iso`: churn is configured or
-// an isolation word was written into the state (raft_engine_write_state).
+// isolation churn without partitions, with config 3's command harness (the
+// lowest LEADER, no limit), or for partitions alone (config 5, and no faults
+// at all: configs 1 and 2), so the other checks are compiled out; otherwise
+// the NET_ALL kernel.  `iso`: churn is configured or an isolation word was
+// written into the state (raft_engine_write_state).
 typedef void (*StepKernel)(DevParams, uint32_t, int);
 template <int R, bool TB, bool RING>
 static StepKernel step_fn(const DevParams& d, const raft_params& p, bool iso) {
     if constexpr (R == 3 || R == 5 || R == 7) {
         const bool drops = d.drop_thr16 != 0, parts = p.partition_period > 0 && p.partition_len > 0;
-        if (drops && !parts) return step_kernel<R, TB, RING, NET_DROP | NET_ISO>;
+        const bool cmdlow = p.cmd_mode == RAFT_CMD_LOWEST_LEADER && p.cmd_limit == 0;
+        if (drops && !parts && cmdlow) return step_kernel<R, TB, RING, NET_DROP | NET_ISO | NET_CMDLOW>;
         if (!drops && !iso) return step_kernel<R, TB, RING, NET_PART>;
     }
     return step_kernel<R, TB, RING, NET_ALL>;

@@ -241,9 +241,12 @@ __device__ __forceinline__ bool no_drops(const DevParams& p) {
 // compiles its checks out (per vote / tick round: the drop compares of both
 // directions, the partition-side extract and compare, or the isolated-sender
 // compare; per step: H's isolation bookkeeping); NET_ALL decides drops at run
-// time.  The host picks the kernel from the engine's raft_params
-// (raft_engine.hip step_fn).
-constexpr int NET_DROP = 1, NET_PART = 2, NET_ISO = 4, NET_ALL = NET_DROP | NET_PART | NET_ISO;
+// time.  NET_CMDLOW: the harness's commands go to the lowest-id LEADER with
+// no per-group limit (cmd_mode LOWEST_LEADER, cmd_limit 0), fixed at compile
+// time instead of two run-time selects per step.  The host picks the kernel
+// from the engine's raft_params (raft_engine.hip step_fn).
+constexpr int NET_DROP = 1, NET_PART = 2, NET_ISO = 4, NET_CMDLOW = 8;
+constexpr int NET_ALL = NET_DROP | NET_PART | NET_ISO;
 // no drop can happen: compile-time in a kernel built without NET_DROP, and
 // at run time (drop_ppm == 0) in a NET_ALL kernel
 template <int NET>
@@ -1366,9 +1369,10 @@ struct Stepper {
         const uint64_t cmd_thr = kp->cmd_thr32;
         if (cmd_thr) {
             const int32_t cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
-            const uint64_t cm = (cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) & lm((uint64_t)hw1 < cmd_thr) &
-                                lm(lead != 0);
-            const uint64_t tgt = cm & (cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
+            constexpr bool CL = (NET & NET_CMDLOW) != 0;                   // lowest LEADER, no limit
+            const uint64_t cm = (CL || cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) &
+                                lm((uint64_t)hw1 < cmd_thr) & lm(lead != 0);
+            const uint64_t tgt = cm & (CL || cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
             append_command<TB, RING>(n.rep(), tgt, c.template log<RING>(p), hw2, cnt);
             n.cmdc = inc_if(n.cmdc, cm);
         }

@@ -10,7 +10,7 @@ d, kn = sys.argv[1], sys.argv[2]
 s = open(f'{d}/raft_engine-hip-amdgcn-amd-amdhsa-gfx950.s').read().split('\n')
 cur = None; st = {}
 for i, l in enumerate(s):
-    m = re.match(r'^(_Z\S*' + kn + r'ILi(\d)ELb(\d)ELb(\d)E(?:Li(\d)E)?\S*):', l)
+    m = re.match(r'^(_Z\S*' + kn + r'ILi(\d)ELb(\d)ELb(\d)E(?:Li(\d+)E)?\S*):', l)
     if m:
         cur = m.group(2) + ("t" if m.group(3) == "1" else "") + ("r" if m.group(4) == "1" else "") + \
               (("/net" + m.group(5)) if m.group(5) else "")

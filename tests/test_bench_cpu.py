@@ -98,7 +98,9 @@ def test_default_launch_length_per_kernel_variant():
     # config 5 (R = 7, partitions, no drops) runs the 7-wave partitions-only kernel
     net5 = abi.step_net_of(abi.CONFIGS[5])
     assert net5 == abi.NET_PART and abi.bench_steps_per_launch(7, abi.MODE_REFERENCE, 0, net5) == 400
-    assert abi.step_net_of(abi.CONFIGS[3]) == abi.NET_DROP | abi.NET_ISO
+    assert abi.step_net_of(abi.CONFIGS[3]) == abi.NET_DROP | abi.NET_ISO | abi.NET_CMDLOW
+    assert abi.step_net_of(dict(abi.CONFIGS[3], cmd_mode=abi.CMD_ALL_LEADERS)) == abi.NET_ALL
+    assert abi.step_net_of(abi.CONFIGS[1]) == abi.NET_PART
     assert abi.step_net_of(abi.CONFIGS[2]) == abi.NET_PART
     assert abi.step_net(5, drop_ppm=1, partition_period=50, partition_len=25) == abi.NET_ALL
     assert abi.step_net(7, partition_period=50, partition_len=25, churn_ppm=1) == abi.NET_ALL

@@ -155,7 +155,8 @@ def test_other_replica_counts(R):
 
 
 NET_CASES = [(3, "drops+churn"), (5, "drops+churn"), (7, "drops+churn"), (5, "drops"), (3, "partitions"),
-             (5, "partitions"), (7, "partitions"), (7, "partitions+churn"), (5, "none"), (5, "churn")]
+             (5, "partitions"), (7, "partitions"), (7, "partitions+churn"), (5, "none"), (5, "churn"),
+             (5, "drops+all-leaders"), (5, "drops+limit")]
 
 
 @pytest.mark.parametrize("R,faults", NET_CASES, ids=[f"{r}-{f}" for r, f in NET_CASES])
@@ -172,9 +173,14 @@ def test_network_fault_kernels(R, faults):
         kw.update(drop_ppm=100_000)
     if "partitions" in faults:
         kw.update(partition_period=40, partition_len=10)
-    want = {"drops+churn": abi.NET_DROP | abi.NET_ISO, "drops": abi.NET_DROP | abi.NET_ISO,
-            "partitions": abi.NET_PART, "none": abi.NET_PART, "partitions+churn": abi.NET_ALL,
-            "churn": abi.NET_ALL}[faults]
+    if "all-leaders" in faults:
+        kw.update(cmd_mode=abi.CMD_ALL_LEADERS)
+    if "limit" in faults:
+        kw.update(cmd_limit=30)
+    low = abi.NET_DROP | abi.NET_ISO | abi.NET_CMDLOW
+    want = {"drops+churn": low, "drops": low, "partitions": abi.NET_PART, "none": abi.NET_PART,
+            "partitions+churn": abi.NET_ALL, "churn": abi.NET_ALL, "drops+all-leaders": abi.NET_ALL,
+            "drops+limit": abi.NET_ALL}[faults]
     assert abi.step_net_of(kw) == want
     e, o = pair(**kw)
     run_lockstep(e, o, 400, 50, f"R={R} {faults}")
