@@ -15,15 +15,15 @@ Multi-GPU: one process per GPU.  With --gpus N > 1 and no torch.distributed
 environment, this script spawns the N rank processes itself (fresh
 interpreters; the parent makes no HIP or torch.cuda call) and exits with their
 status.  Groups never talk across GPUs, so the path shards with no data-path
-exchange: by default every GPU runs its own 10^6 groups (weak scaling,
-contiguous global-id ranges, `value` = every rank's group-steps / the MAX of
-the ranks' times).  The line then also carries `config4_strong`, BASELINE.json
-configs[3] measured in the same job: 10^6 groups split into contiguous
-global-id ranges over the N GPUs, timed the same way, whose all-reduced
-counter rows must equal rank 0's weak-shard rows (the same global groups).
---scaling strong makes that split the main measurement.  The only collective is
-the all-reduce of the per-step counter rows over RCCL, batched on a side
-stream.  Rank 0 prints ONE JSON line.
+exchange.  By default `value` is BASELINE.json configs[3] ("config 4"): the
+same 10^6 groups split into contiguous global-id ranges over the N GPUs
+(strong scaling, `value` = 10^6 x steps / the MAX of the ranks' times).  The
+line then also carries `weak_scaling`, measured in the same job: every GPU its
+own 10^6 groups, timed the same way, whose rank-0 counter rows must equal the
+strong leg's all-reduced rows (the same global groups).  --scaling weak swaps
+the two (the strong leg is then `config4_strong`).  The only collective is the
+all-reduce of the per-step counter rows over RCCL, batched on a side stream.
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -56,6 +56,7 @@ REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
 GROUP_BYTES = 4 * 3
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
 KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h")
+SCHEDULES = {"auto": abi.SCHED_AUTO, "one": abi.SCHED_ONE_PER_WAVE, "balanced": abi.SCHED_BALANCED}
 
 
 def kernel_source_id() -> str:
@@ -246,11 +247,12 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--groups", type=int, default=1_000_000,
                     help="total groups (strong scaling) or groups per GPU (weak scaling)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: --groups per GPU (the path shards with no exchange); strong: --groups split over "
-                         "the GPUs (config 4)")
-    ap.add_argument("--no-strong-leg", action="store_true",
-                    help="N > 1, weak scaling: skip the config-4 strong-shard leg")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong (config 4, BASELINE.json configs[3]): --groups split over the GPUs; weak: --groups "
+                         "per GPU")
+    ap.add_argument("--no-side-leg", "--no-strong-leg", dest="no_side_leg", action="store_true",
+                    help="N > 1, config 3: skip the other scaling's leg (weak beside a strong job, strong beside a "
+                         "weak one)")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     ap.add_argument("--mode", choices=["reference", "textbook"], default="reference",
                     help="protocol mode: the reference's handlers (parity) or the opt-in textbook rules")
@@ -261,6 +263,9 @@ def parse_args(argv=None):
                          "0 = the kernel variant's default (abi.bench_steps_per_launch)")
     ap.add_argument("--subranges", type=int, default=0,
                     help="step-kernel launch sub-ranges, each on its own stream (0 = the engine's automatic choice)")
+    ap.add_argument("--schedule", choices=["auto", "one", "balanced"], default="auto",
+                    help="step-kernel schedule (raft_params.schedule): balanced when the chunks outnumber the "
+                         "resident wave slots (auto), one chunk per wave, or balanced")
     ap.add_argument("--stream-steps", type=int, default=200,
                     help="steps of the streaming leg (1 step per launch: the HBM-bound formulation)")
     ap.add_argument("--log-cap", type=int, default=0)
@@ -550,21 +555,24 @@ def timed_leg(eng, args, chunk, coll, dev, world):
             "counters": counters, "gcounters": gcounters, "wcount": wcount}
 
 
-def strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, weak_rows0):
-    """BASELINE.json configs[3] (config 4) inside an N > 1 weak-scaling job:
-    --groups groups split into contiguous global-id ranges over the ranks,
-    warmed up and timed exactly like the main leg (timed_leg).  Rank 0's weak
-    shard holds the same global groups 0..groups-1, so the strong leg's
-    all-reduced counter rows must equal rank 0's weak rows (`weak_rows0`)."""
+def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, scaling, main_rows):
+    """The other scaling's leg of an N > 1 config-3 job, warmed up and timed
+    exactly like the main leg (timed_leg).  Rank 0's weak shard holds global
+    groups 0..groups-1, which the strong split covers over all ranks, so the
+    strong leg's all-reduced counter rows must equal rank 0's weak-shard rows:
+    beside a strong job (the default) this leg is weak scaling (every GPU its
+    own --groups groups) and `main_rows` are the strong leg's all-reduced rows;
+    beside a weak job it is config 4 (`main_rows`: rank 0's weak rows)."""
     eng_mod = importlib.import_module("raft-kotlin_amd.engine")
     import torch
     R = kw["R"]
-    g0, G = shard(args.groups, world, rank, "strong")
-    per_rank = [shard(args.groups, world, q, "strong")[1] for q in range(world)]
+    g0, G = shard(args.groups, world, rank, scaling)
+    per_rank = [shard(args.groups, world, q, scaling)[1] for q in range(world)]
+    total = sum(per_rank)
     flat = -(-G // (64 // R)) * 64 * log_cap * 8
     window = 0 if flat <= 0.6 * torch.cuda.get_device_properties(dev).total_memory else 256
     params = abi.make_params(log_cap=max(log_cap, window), log_window=window, steps_per_launch=L, mode=mode,
-                             subranges=args.subranges or (1 if args.steps <= L else 0),
+                             subranges=args.subranges, schedule=SCHEDULES[args.schedule],
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges
@@ -573,11 +581,12 @@ def strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk,
     finally:
         eng.close()
     c_all = leg["gcounters"].cpu().numpy()[:, : abi.NUM_COUNTERS]
+    c_loc = leg["counters"].cpu().numpy()[:, : abi.NUM_COUNTERS]
     wc = leg["wcount"].cpu().numpy()[: args.warmup, : abi.NUM_COUNTERS]
     bad = int(c_all[:, abi.C_INDEX["log_overflow"]].sum() + c_all[:, abi.C_INDEX["log_window_miss"]].sum()
               + wc[:, abi.C_INDEX["log_overflow"]].sum() + wc[:, abi.C_INDEX["log_window_miss"]].sum())
-    out = {"value": args.groups * args.steps / leg["elapsed"], "unit": "group-steps/s", "scaling": "strong",
-           "ms_per_step": leg["elapsed"] * 1e3 / args.steps, "groups_total": args.groups, "groups_per_rank": per_rank,
+    out = {"value": total * args.steps / leg["elapsed"], "unit": "group-steps/s", "scaling": scaling,
+           "ms_per_step": leg["elapsed"] * 1e3 / args.steps, "groups_total": total, "groups_per_rank": per_rank,
            "steps_per_launch": L, "subranges": nsub, "log_window": window,
            "step_waves_per_rank": -(-G // (64 // R)),
            "grid_fill": grid_fill(G, R, L, abi.bench_steps_per_launch(R, mode, window, abi.step_net_of(kw))
@@ -585,12 +594,20 @@ def strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk,
            "kernel_avg_ms_per_rank": leg["kern_avg_per_rank"],
            "timing": {"wall_ms": leg["wall"] * 1e3, "stream_event_ms": leg["ev_ms"],
                       "step_kernel_ms_total": leg["kern_ms"]},
-           "valid": bad == 0,
-           "note": "config 4 in the same job: the groups split by contiguous global id over the GPUs, the same "
-                   "steps, warmup and timing as the main leg; counters_equal_rank0_weak_shard: its all-reduced "
-                   "per-step counter rows equal rank 0's weak-leg rows, which cover the same global groups"}
-    if weak_rows0 is not None:
-        out["counters_equal_rank0_weak_shard"] = bool(np.array_equal(c_all, weak_rows0))
+           "valid": bad == 0}
+    if scaling == "weak":
+        out["note"] = ("weak scaling in the same job: every GPU its own --groups groups (contiguous global-id "
+                       "ranges), the same steps, warmup and timing as the main leg; "
+                       "counters_equal_strong_allreduced: rank 0's rows (global groups 0..groups-1) equal the "
+                       "strong leg's all-reduced rows, which cover the same groups")
+        if main_rows is not None:
+            out["counters_equal_strong_allreduced"] = bool(np.array_equal(c_loc, main_rows))
+    else:
+        out["note"] = ("config 4 in the same job: the groups split by contiguous global id over the GPUs, the same "
+                       "steps, warmup and timing as the main leg; counters_equal_rank0_weak_shard: its all-reduced "
+                       "per-step counter rows equal rank 0's weak-leg rows, which cover the same global groups")
+        if main_rows is not None:
+            out["counters_equal_rank0_weak_shard"] = bool(np.array_equal(c_all, main_rows))
     return out
 
 
@@ -679,12 +696,11 @@ def main(argv=None, result=None):
     spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window, net)
     L = launch_length(args.steps, spl)                      # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
-    # launch sub-ranges: the engine's automatic choice overlaps one range's
-    # last waves with another's next launch; a timed region of ONE launch has
-    # no next launch to overlap, and there one full-grid dispatch is faster
-    # (DESIGN.md §6), so --subranges 0 resolves to 1 for it
-    subranges = args.subranges or (1 if args.steps <= L else 0)
+    # launch sub-ranges: 0 = the engine's automatic choice (one: the balanced
+    # schedule ends a launch's waves together)
+    subranges = args.subranges
     params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=subranges,
+                             schedule=SCHEDULES[args.schedule],
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs
@@ -796,13 +812,14 @@ def main(argv=None, result=None):
                 "properties); over the timed steps, Log Matching at the end of the run",
     }
 
-    # config 4 (the 10^6 groups split over the GPUs) beside a weak-scaling job
-    strong = None
-    if world > 1 and args.scaling == "weak" and args.config == 3 and not args.no_strong_leg:
+    # the other scaling's leg: weak beside config 4 (the default), config 4 beside a weak job
+    side = None
+    if world > 1 and args.config == 3 and not args.no_side_leg:
         eng.close()
         eng = None
-        strong = strong_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk,
-                            c_loc if rank == 0 else None)
+        other = "weak" if args.scaling == "strong" else "strong"
+        side = side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, other,
+                        (c_all if other == "weak" else c_loc) if rank == 0 else None)
 
     cfg_name = "config4" if world > 1 and args.config == 3 and args.scaling == "strong" else f"config{args.config}"
     out = {
@@ -870,8 +887,8 @@ def main(argv=None, result=None):
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
     }
-    if strong is not None:
-        out["config4_strong"] = strong
+    if side is not None:
+        out["weak_scaling" if side["scaling"] == "weak" else "config4_strong"] = side
     if args.handler_batch > 0 and world == 1 and not coll:
         out["handler_batch"] = handler_batch_leg(eng, args, dict(kw, mode=mode, ae_max_entries=args.ae_max_entries),
                                                  log_cap, dev, G_local, R)

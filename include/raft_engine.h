@@ -40,7 +40,9 @@
 extern "C" {
 #endif
 
-#define RAFT_ABI_VERSION 1
+/* 2: raft_params.schedule / schedule_workgroups, automatic subranges = 1,
+ * raft_engine_kernel_info */
+#define RAFT_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
 #define RAFT_OK            0
@@ -118,14 +120,46 @@ typedef struct raft_params {
                                  * (greeter.proto:37 `repeated LogEntry entries`).  0 or 1 = one
                                  * entry, the reference's shape (RaftServer.kt:130-132); at most
                                  * RAFT_MAX_AE_ENTRIES.  Must be 0 or 1 in reference mode.       */
-    int32_t  subranges;         /* engine only: the step kernel's workgroups split into this many
-                                 * contiguous ranges, each launched on its own stream, so that one
-                                 * range's last waves overlap another's next launch (a launch
-                                 * boundary otherwise leaves the chip part-empty while its last
-                                 * waves finish).  0 = automatic (raft_engine_subranges reports the
-                                 * choice), 1..RAFT_MAX_SUBRANGES.  Results never depend on it.     */
-    int32_t  reserved[3];
+    int32_t  subranges;         /* engine only: the step kernel's chunks (waves of groups) split into
+                                 * this many contiguous ranges, each launched on its own stream, so
+                                 * that one range's last waves can overlap another's next launch.
+                                 * 0 = automatic = 1 (ABI 2; ABI 1 chose 3: the balanced schedule
+                                 * below ends every wave of a launch together, so one range is
+                                 * enough), 1..RAFT_MAX_SUBRANGES.  Results never depend on it.    */
+    int32_t  schedule;          /* engine only: RAFT_SCHED_* (0 = automatic).  Results never depend
+                                 * on it.                                                          */
+    int32_t  schedule_workgroups; /* engine only: workgroups of a balanced launch (0 = as many as
+                                 * the GPU holds at once at the launch's LDS; tests set fewer)     */
+    int32_t  reserved[1];
 } raft_params;
+
+/* ---- step-kernel schedules (raft_params.schedule) --------
+ * A chunk is one wave's 64 / R groups.  ONE_PER_WAVE launches a wave per
+ * chunk for all steps of the launch: when the chunks outnumber the GPU's
+ * resident wave slots, the last round of waves runs on a part-empty chip.
+ * BALANCED launches only the workgroups the GPU holds at once; each takes a
+ * contiguous run of chunks and its waves split the run's chunk-steps into
+ * equal parts (a chunk may pass from one wave to the next between steps),
+ * so every wave ends together.  AUTO takes BALANCED when the chunks
+ * outnumber the resident wave slots, else ONE_PER_WAVE. */
+#define RAFT_SCHED_AUTO         0
+#define RAFT_SCHED_ONE_PER_WAVE 1
+#define RAFT_SCHED_BALANCED     2   /* whenever every workgroup gets >= 4 chunks */
+
+/* What the last step launch ran (raft_engine_kernel_info). */
+typedef struct raft_kernel_info {
+    int32_t net;                 /* network faults the kernel was built for: bit 0 drops, 1 partitions,
+                                  * 2 isolation churn, 3 config 3's command harness compiled in
+                                  * (raft_step.h NET_*)                                              */
+    int32_t textbook;            /* 1: RAFT_MODE_TEXTBOOK kernel                                   */
+    int32_t ring;                /* 1: the log_window ring kernel                                  */
+    int32_t steps;               /* steps of the launch                                            */
+    int32_t workgroups;          /* workgroups of the launch, all sub-ranges                       */
+    int32_t resident_workgroups; /* workgroups of this kernel the GPU holds at once at that LDS    */
+    int32_t balanced;            /* sub-ranges that ran the balanced schedule                      */
+    int32_t subranges;           /* sub-ranges (streams) of the launch                             */
+    int32_t reserved[4];
+} raft_kernel_info;
 
 /* ---- per-step counters (sum over the engine's groups) ------------------ */
 enum raft_counter {
@@ -250,6 +284,8 @@ int     raft_engine_set_steps_per_launch(raft_engine* e, int32_t k);
 /* Launch sub-ranges from now on (raft_params.subranges; 0 = automatic). */
 int     raft_engine_set_subranges(raft_engine* e, int32_t n);
 int32_t raft_engine_subranges(raft_engine* e);    /* the sub-ranges in use (-1: null engine) */
+/* The step kernel and schedule of the last step launch (zeros before the first). */
+int     raft_engine_kernel_info(raft_engine* e, raft_kernel_info* out);
 /* Set the index of the next step (its Philox counter c0); with write_state
  * this resumes a run exported at any step. */
 int     raft_engine_set_step_index(raft_engine* e, int64_t t);
@@ -306,10 +342,18 @@ void* raft_host_alloc(int64_t bytes);
 int   raft_host_free(void* p);
 /* The same three on DEVICE buffers of this engine's GPU (group, dst/replica,
  * req, resp: n entries each, in HBM), enqueued on the engine stream; they
- * return once the batch finished.  The host entry points above stage their
- * buffers through engine-owned pinned memory and call these.  A message whose
- * group or replica is outside the engine makes the whole batch fail with
- * RAFT_ERANGE before any message is applied.  n < 2^31. */
+ * return once the batch finished.  The engine stream is non-blocking: it does
+ * NOT wait for work on other streams, so the device buffers must be complete
+ * (and resp no longer in use) before the call -- produced on the engine
+ * stream, synchronised, or ordered with raft_engine_wait_stream().  The host
+ * entry points above stage their buffers through engine-owned pinned memory
+ * and call these.  A message whose group or replica is outside the engine
+ * makes the whole batch fail with RAFT_ERANGE before any message is applied.
+ * n < 2^31. */
+/* Order the engine stream after all work enqueued so far on `stream` (a
+ * hipStream_t as void*, NULL = the null stream): later engine calls see that
+ * work's results.  Host-side and non-blocking (an event record and wait). */
+int raft_engine_wait_stream(raft_engine* e, void* stream);
 int raft_vote_batch_dev(raft_engine* e, const int64_t* group, const int32_t* dst,
                         const raft_vote_req* req, raft_vote_resp* resp, int64_t n);
 int raft_append_batch_dev(raft_engine* e, const int64_t* group, const int32_t* dst,

@@ -115,8 +115,19 @@ class raft_params(C.Structure):
         ("partition_period", C.c_int32), ("partition_len", C.c_int32),
         ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
         ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("log_window", C.c_int32),
-        ("ae_max_entries", C.c_int32), ("subranges", C.c_int32), ("reserved", C.c_int32 * 3),
+        ("ae_max_entries", C.c_int32), ("subranges", C.c_int32), ("schedule", C.c_int32),
+        ("schedule_workgroups", C.c_int32), ("reserved", C.c_int32 * 1),
     ]
+
+
+# step-kernel schedules (raft_params.schedule)
+SCHED_AUTO, SCHED_ONE_PER_WAVE, SCHED_BALANCED = 0, 1, 2
+
+
+class raft_kernel_info(C.Structure):
+    _fields_ = [("net", C.c_int32), ("textbook", C.c_int32), ("ring", C.c_int32), ("steps", C.c_int32),
+                ("workgroups", C.c_int32), ("resident_workgroups", C.c_int32), ("balanced", C.c_int32),
+                ("subranges", C.c_int32), ("reserved", C.c_int32 * 4)]
 
 
 class raft_vote_req(C.Structure):
@@ -231,6 +242,8 @@ def load_library(path: str | None = None):
         "raft_engine_set_steps_per_launch": (C.c_int, [eng, I32]),
         "raft_engine_set_subranges": (C.c_int, [eng, I32]),
         "raft_engine_subranges": (I32, [eng]),
+        "raft_engine_kernel_info": (C.c_int, [eng, P(raft_kernel_info)]),
+        "raft_engine_wait_stream": (C.c_int, [eng, C.c_void_p]),
         "raft_engine_device_bytes": (I64, [eng]),
         "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
         "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
@@ -280,7 +293,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
-    "raft_engine_set_subranges", "raft_engine_subranges",
+    "raft_engine_set_subranges", "raft_engine_subranges", "raft_engine_kernel_info", "raft_engine_wait_stream",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",

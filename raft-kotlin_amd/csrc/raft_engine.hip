@@ -51,7 +51,9 @@ constexpr int STEP_BLOCK = RAFT_STEP_BLOCK;
 constexpr int STEP_WAVES = STEP_BLOCK / 64;
 constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
 constexpr int TALLY_LDS_WORDS = STEP_WAVES * 16;          // per-wave vote-tally words (Ctx::tl, R >= 4)
-constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS;
+constexpr int FLAG_LDS_WORDS = STEP_WAVES;                // balanced schedule: a wave's head piece is stored
+constexpr int PLAN_LDS_WORDS = STEP_WAVES * 4;            // each wave's plan (plan_of)
+constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS + FLAG_LDS_WORDS + PLAN_LDS_WORDS;
 // the longest launch whose LDS (job rows, tally words, K counter rows) still
 // lets 7 step workgroups share a CU's 160 KB
 constexpr int STEP_K_7WG = (160 * 1024 / 7 / 4 - PRE_CNT_LDS_WORDS) / NCW;
@@ -185,30 +187,126 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 #endif
 // NET: the network faults the kernel is built for (raft_step.h NET_DROP /
 // NET_PART; the host's step_fn picks it from raft_params).
+//
+// The launch's schedule.  A chunk is one wave's worth of groups (GPW, one log
+// block); a piece is (chunk, steps [k0, k1)): load the chunk's replicas, run
+// those steps, store them back -- exactly a launch boundary, which results
+// never depend on.
+//  * One chunk per wave (bal_chunks == 0): chunk wave0 + blockIdx.x *
+//    STEP_WAVES + wave, all steps; the grid has a wave per chunk.  When the
+//    chunks outnumber the chip's resident wave slots, the last round of waves
+//    runs on a part-empty chip (1.25e5 groups: 10,417 waves = 1.45 rounds of
+//    the 7,168 slots).
+//  * Balanced (bal_chunks > 0): the grid is the workgroups the chip holds at
+//    once; workgroup b takes the chunks [b * n / nb, (b + 1) * n / nb) (n =
+//    bal_chunks, nb = gridDim.x, at least STEP_WAVES of them) and its waves
+//    split the m chunks' m * K chunk-steps into equal quarters (McNaughton's
+//    wrap-around rule).  A quarter [u0, u1) is a head piece (the first e steps
+//    of the chunk it ends in), whole chunks, and a tail piece (the last K - s
+//    steps of the chunk it starts in, whose first s steps are the previous
+//    wave's head).  A wave runs its head FIRST and its tail LAST, so the tail
+//    starts (at >= K chunk-steps into the wave's quarter, which is >= K long)
+//    after the previous wave's head ended (at <= K): the one dependency, wave
+//    w's tail on wave w - 1's head, is an in-workgroup hand-off through an
+//    LDS flag (both waves on one CU, always co-resident; no other workgroup
+//    is involved, so dispatch order and XCD placement do not matter).  Every
+//    wave then ends within one chunk-step of the others.
+struct Piece {
+    int32_t chunk, k0, k1;
+    bool wait;                    // tail: wait until the previous wave has stored its head
+    bool signal;                  // head: tell the next wave it is stored
+};
+// A wave's plan, 4 words (made once per launch by plan_of, kept in LDS and
+// read back at each piece boundary, so the step loop carries no schedule
+// arithmetic): the head's steps e (0: none), the first whole chunk f, the
+// whole chunks nf, the tail's first step s (0: none).  The head is chunk
+// f + nf, the tail chunk f - 1.
+__device__ __forceinline__ uint4 plan_of(int wib, int K) {
+    const KernArgs kp = kernargs();
+    if (kp->bal_chunks == 0)
+        return make_uint4(0u, (uint32_t)(kp->wave0 + (int32_t)blockIdx.x * STEP_WAVES + wib), 1u, 0u);
+    // workgroup b: chunks [c0, c0 + m), m = q or q + 1 (q = n / nb, the first
+    // n % nb workgroups take one more); 32-bit throughout (the host keeps
+    // m * K < 2^31)
+    const uint32_t b = blockIdx.x, q = (uint32_t)kp->bal_q, rem = (uint32_t)kp->bal_rem, k = (uint32_t)K;
+    const uint32_t c0 = (uint32_t)kp->wave0 + b * q + min(b, rem);
+    const uint32_t U = (q + (b < rem ? 1u : 0u)) * k;
+    const uint32_t u0 = (uint32_t)wib * U / STEP_WAVES, u1 = (uint32_t)(wib + 1) * U / STEP_WAVES;
+    const uint32_t a = u0 / k, s = u0 - a * k, z = u1 / k, e = u1 - z * k;
+    const uint32_t f = a + (s != 0);
+    return make_uint4(e, c0 + f, z - f, s);
+}
+__device__ __forceinline__ int n_pieces(uint4 pl) { return (pl.x != 0) + (int)pl.z + (pl.w != 0); }
+__device__ __forceinline__ Piece piece_of(uint4 pl, int q, int K) {
+    const int32_t e = (int32_t)pl.x, f = (int32_t)pl.y, nf = (int32_t)pl.z, s = (int32_t)pl.w;
+    if (e != 0) {
+        if (q == 0) return Piece{f + nf, 0, e, false, true};                       // head
+        --q;
+    }
+    if (q < nf) return Piece{f + q, 0, K, false, false};                           // whole chunks
+    return Piece{f - 1, s, K, true, false};                                        // tail
+}
+// Bounded wait for the previous wave's head piece (never reached by a correct
+// schedule without the flag set; the bound keeps a broken one from hanging the
+// GPU -- its results would then differ from the oracle's).  The flag is set
+// after the producer's stores completed (vmcnt(0)); the producer is on this CU,
+// whose vector L1 is invalidated here before the chunk's state is read.
+__device__ __forceinline__ void wait_head(const uint32_t* flag) {
+    for (uint32_t spins = 0; spins < (1u << 24); ++spins) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    asm volatile("buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Enter a piece: chunk `wid`'s replicas into VGPRs.  The lane geometry comes
+// from the context (lane = base + r, group j = base / R) and the parameters
+// from the kernarg segment: kept live across the step loop for the next
+// piece's entry, they would pin registers (kernargs()).
+template <int R, bool RING>
+__device__ __forceinline__ void enter_piece(Ctx<R>& c, Node& n, int wid) {
+    using L = Lanes<R>;
+    const KernArgs kp = kernargs();
+    DevParams p;
+    p.st = kp->st; p.ses = kp->ses; p.gx = kp->gx; p.GR = kp->GR; p.G = kp->G;
+    const int j = (int)c.j();
+    const int64_t g = (int64_t)wid * L::GPW + j;
+    c.live = j < L::GPW && g < p.G;
+    c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
+    c.gg0 = (uint32_t)(kp->g0 + c.wg0);
+    c.lr = kp->log + ((int64_t)wid * 64 + c.base + c.r) * (RING ? kp->nslots : kp->cap);   // its chunk's block, its row
+    if (c.live) load_node(n, p, g, g * R + c.r);
+    else inert_node(n);
+    c.lead = c.gbits(__ballot(n.role == RAFT_LEADER));                  // Stepper::step's lead0 of the first step
+    // Drain the state loads here: left pending into the loop, they make the
+    // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
+    // previous step's log stores, so each step would start by waiting for them.
+    __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
+}
+
 template <int R, bool TB, bool RING, int NET>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU(R, TB, RING, NET))))
 void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     using L = Lanes<R>;
-    // LDS: [STEP_WAVES][64][4] the step's Philox job words (Ctx::jl),
-    // then the counter rows [nsteps][NCW]
+    // LDS: [STEP_WAVES][64][4] the step's Philox job words (Ctx::jl), the
+    // tally words, the head-piece flags, then the counter rows [nsteps][NCW]
     extern __shared__ uint32_t lds[];
     uint32_t* const lds_cnt = lds + PRE_CNT_LDS_WORDS;
+    uint32_t* const lds_flag = lds + JOB_LDS_WORDS + TALLY_LDS_WORDS;
+    uint32_t* const lds_plan = lds_flag + FLAG_LDS_WORDS;
     const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-    const int wid = p.wave0 + blockIdx.x * STEP_WAVES + wib;              // wave0: this launch's sub-range
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: the schedule's loop is uniform
     const int j = lane / R;
     const int r = lane - j * R;
-    const int64_t g = (int64_t)wid * L::GPW + j;
-    const bool live = j < L::GPW && g < p.G;
+
+    for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
+    if (threadIdx.x < FLAG_LDS_WORDS) lds_flag[threadIdx.x] = 0u;
+    __syncthreads();                                                      // counter rows and flags zeroed
 
     Ctx<R> c;
     c.r = r;
     c.base = j * R;
-    c.live = live;
-    c.wg0 = (uint32_t)__builtin_amdgcn_readfirstlane(wid * L::GPW);
-    c.gg0 = (uint32_t)(p.g0 + c.wg0);
-    const int64_t idx = g * R + r;
-    c.lr = p.log + ((int64_t)wid * 64 + lane) * (RING ? p.nslots : p.cap);   // its wave's block, its row
     c.iso = -1;
     c.iso_me = 0;
     c.part = 0;
@@ -217,19 +315,24 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     c.tw = c.dwt = c.dwv = 0u;
     c.jl = lds + wib * 256;
     c.tl = lds + JOB_LDS_WORDS + wib * 16;
-
-    for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
-    Node n;
     c.clk.start();
-    if (live) load_node(n, p, g, idx);
-    else inert_node(n);
-    c.lead = c.gbits(__ballot(n.role == RAFT_LEADER));                  // Stepper::step's lead0 of the first step
-    // Drain the state loads here: left pending into the loop, they make the
-    // loop header wait on vmcnt(0) every step -- and vmcnt also counts the
-    // previous step's log stores, so each step would start by waiting for them.
-    __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
-    __syncthreads();                                                      // counter rows zeroed
-    for (int k = 0; k < nsteps; ++k) {
+    Node n;
+    // One loop over the wave's chunk-steps; a piece boundary (the launch's
+    // end in the one-chunk-per-wave schedule) is a rare branch in it that
+    // stores the chunk and loads the next.  (A loop over pieces around the
+    // step loop made the compiler hoist and duplicate: 76 B of scratch and
+    // +600 static VALU at R = 5.)
+    int pc = 0;                                    // this wave's current piece
+    int k, k1, k0;                                 // its step, the step it ends before, its first step
+    {   // (a wave's first piece is never a tail: a wave runs its head first)
+        const uint4 pl = plan_of(wib, nsteps);
+        *(uint4*)(lds_plan + wib * 4) = pl;
+        const Piece pz = piece_of(pl, 0, nsteps);
+        enter_piece<R, RING>(c, n, pz.chunk);
+        k = k0 = pz.k0;
+        k1 = pz.k1;
+    }
+    for (;;) {
         const uint32_t t = t0 + (uint32_t)k;
         c.t = t;
         // The lane geometry (r, base) is carried across steps behind an opaque
@@ -251,7 +354,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             if (pperiod > 0) {                                            // S-11 partitions
                 const uint32_t ph = t % (uint32_t)pperiod;
                 if ((int64_t)ph < kp->part_len) {
-                    if (k == 0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
+                    if (k == k0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
                 } else {
                     c.part = 0;
                 }
@@ -271,7 +374,37 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         if (ib((1ull << NCW) - 1))
             __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         c.clk.mark(PH_CNT);
+        if (++k == k1) {                           // the piece ends: store its chunk (rare)
+            if (c.live) {
+                const KernArgs kp = kernargs();    // state pointers re-read, not kept live across the loop
+                DevParams q;
+                q.st = kp->st; q.ses = kp->ses; q.gx = kp->gx; q.GR = kp->GR; q.G = kp->G;
+                store_node(n, q, (int64_t)c.wg0 + j, c.idx(), r == 0);
+            }
+            // this wave's index from its job rows' address (kept live across
+            // the loop, the index would pin a register)
+            const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
+            uint4 pl = *(const uint4*)(lds_plan + wb * 4);
+            pl.x = __builtin_amdgcn_readfirstlane(pl.x);        // one word for the whole wave
+            pl.y = __builtin_amdgcn_readfirstlane(pl.y);
+            pl.z = __builtin_amdgcn_readfirstlane(pl.z);
+            pl.w = __builtin_amdgcn_readfirstlane(pl.w);
+            if (pc == 0 && pl.x != 0) {            // a head stored: the next wave's tail may load it
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(lds_flag + wb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (++pc == n_pieces(pl)) break;
+            const Piece pz = piece_of(pl, pc, nsteps);
+            if (pz.wait) wait_head(lds_flag + wb - 1);
+            enter_piece<R, RING>(c, n, pz.chunk);
+            k = k0 = pz.k0;
+            k1 = pz.k1;
+        }
     }
+#ifdef RAFT_PROFILE_PHASES
+    if (lane == 0)
+        for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
+#endif
     __syncthreads();
     {   // workgroup partials; the launch's partials geometry re-read from the
         // kernarg segment (held across the step loop it would pin SGPRs)
@@ -279,16 +412,6 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         uint32_t* const part = kp->part + kp->part_col0 + blockIdx.x;
         const int64_t stride = kp->part_stride;
         for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) part[(int64_t)q * stride] = lds_cnt[q];
-    }
-#ifdef RAFT_PROFILE_PHASES
-    if (lane == 0)
-        for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
-#endif
-    if (live) {
-        const KernArgs kp = kernargs();            // state pointers re-read, not kept live across the loop
-        DevParams q;
-        q.st = kp->st; q.ses = kp->ses; q.gx = kp->gx; q.GR = kp->GR; q.G = kp->G;
-        store_node(n, q, g, c.idx(), r == 0);
     }
 }
 
@@ -698,7 +821,15 @@ struct raft_engine {
     size_t bytes;
     uint64_t t;
     int K;                      // steps per launch
-    int nblocks;                // step-kernel workgroups: ceil(G / (STEP_WAVES * (64 / R)))
+    int nwaves;                 // chunks: ceil(G / (64 / R)), one wave's groups (and log block) each
+    int nblocks;                // step-kernel workgroups of the one-chunk-per-wave schedule: ceil(nwaves / STEP_WAVES)
+    int ncu;                    // compute units of the device
+    // the launch schedule (raft_params.schedule, schedule_workgroups; step_kernel)
+    int schedule, sched_wg;
+    raft_kernel_info last;      // the last step launch (raft_engine_kernel_info)
+    const void* occ_kern;       // workgroups per CU of occ_kern at occ_lds bytes of LDS (cached)
+    size_t occ_lds;
+    int occ_wg;
     uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials (buffer 0)
     uint32_t* partials2;        // buffer 1: launches alternate between the two when nsub > 1
     // launch sub-ranges (raft_engine_step_async): the step workgroups split
@@ -709,6 +840,7 @@ struct raft_engine {
     int sub_b0[RAFT_MAX_SUBRANGES + 1];       // workgroup boundaries
     hipStream_t sub_stream[RAFT_MAX_SUBRANGES];
     hipEvent_t ev_fork, ev_sub_done[RAFT_MAX_SUBRANGES], ev_red_done[2];
+    hipEvent_t ev_wait;         // raft_engine_wait_stream
     uint64_t launches_issued;   // step launches (all sub-ranges) so far: the partials buffer parity
     bool fork_needed;           // the engine stream holds work the sub-range streams have not waited for
     // batch path staging, grow-only: device scratch (keys, sort), device
@@ -723,7 +855,6 @@ struct raft_engine {
     char* aux;                  // device staging of the state / log / digest accessors, grow-only
     size_t aux_bytes;
     int64_t* counters_dev;      // [K][STRIDE] scratch
-    int nchunks;                // counter-reduction chunks of REDUCE_CHUNK partials
     unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
     // step-kernel event timing
     bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
@@ -736,6 +867,9 @@ struct raft_engine {
 
 template <template <int> class Fn, typename... A>
 static void dispatch_R(int R, A&&... a) {
+#ifdef RAFT_ISA_ONLY_R              // ISA inspection builds (scripts/isa_stats.sh): one R only
+    if (R == RAFT_ISA_ONLY_R) Fn<RAFT_ISA_ONLY_R>::run(a...);
+#else
     switch (R) {
         case 1: Fn<1>::run(a...); break;
         case 2: Fn<2>::run(a...); break;
@@ -747,6 +881,7 @@ static void dispatch_R(int R, A&&... a) {
         case 8: Fn<8>::run(a...); break;
         default: break;
     }
+#endif
 }
 
 template <int R> struct InitL {
@@ -763,35 +898,96 @@ template <int R> struct InitL {
 // the NET_ALL kernel.  `iso`: churn is configured or an isolation word was
 // written into the state (raft_engine_write_state).
 typedef void (*StepKernel)(DevParams, uint32_t, int);
+static int step_net(const DevParams& d, const raft_params& p, int R, bool iso) {
+    if (R == 3 || R == 5 || R == 7) {
+        const bool drops = d.drop_thr16 != 0, parts = p.partition_period > 0 && p.partition_len > 0;
+        const bool cmdlow = p.cmd_mode == RAFT_CMD_LOWEST_LEADER && p.cmd_limit == 0;
+        if (drops && !parts && cmdlow) return NET_DROP | NET_ISO | NET_CMDLOW;
+        if (!drops && !iso) return NET_PART;
+    }
+    return NET_ALL;
+}
 template <int R, bool TB, bool RING>
 static StepKernel step_fn(const DevParams& d, const raft_params& p, bool iso) {
     if constexpr (R == 3 || R == 5 || R == 7) {
-        const bool drops = d.drop_thr16 != 0, parts = p.partition_period > 0 && p.partition_len > 0;
-        const bool cmdlow = p.cmd_mode == RAFT_CMD_LOWEST_LEADER && p.cmd_limit == 0;
-        if (drops && !parts && cmdlow) return step_kernel<R, TB, RING, NET_DROP | NET_ISO | NET_CMDLOW>;
-        if (!drops && !iso) return step_kernel<R, TB, RING, NET_PART>;
+        const int net = step_net(d, p, R, iso);
+        if (net == (NET_DROP | NET_ISO | NET_CMDLOW)) return step_kernel<R, TB, RING, NET_DROP | NET_ISO | NET_CMDLOW>;
+        if (net == NET_PART) return step_kernel<R, TB, RING, NET_PART>;
     }
     return step_kernel<R, TB, RING, NET_ALL>;
 }
-template <int R> struct StepL {
-    static void run(raft_engine* e, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st, int b0, int b1,
-                    uint32_t* partials) {
-        const size_t lds = (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4;
+template <int R> struct KernL {
+    static void run(raft_engine* e, StepKernel* out) {
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
         const bool iso = e->dp.churn_thr32 != 0 || e->iso_written;
-        auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK
-                         ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p, iso)
-                                            : step_fn<R, true, false>(e->dp, e->p, iso))
-                         : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p, iso)
-                                            : step_fn<R, false, false>(e->dp, e->p, iso));
+        *out = e->p.mode == RAFT_MODE_TEXTBOOK
+                   ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p, iso)
+                                      : step_fn<R, true, false>(e->dp, e->p, iso))
+                   : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p, iso)
+                                      : step_fn<R, false, false>(e->dp, e->p, iso));
+    }
+};
+static StepKernel step_kernel_of(raft_engine* e) {
+    StepKernel k = nullptr;
+    dispatch_R<KernL>(e->p.R, e, &k);
+    return k;
+}
+static size_t step_lds_bytes(int k) { return (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4; }
+
+// One launch's geometry over the sub-ranges: sub-range q covers the chunks
+// [w0[q], w0[q + 1]) with nb[q] workgroups, balanced (bal[q] = its chunks) or
+// one chunk per wave (bal[q] = 0), and writes partial columns [col0[q],
+// col0[q] + nb[q]) of a launch with `stride` columns.
+struct LaunchGeo {
+    int w0[RAFT_MAX_SUBRANGES + 1], nb[RAFT_MAX_SUBRANGES], col0[RAFT_MAX_SUBRANGES], bal[RAFT_MAX_SUBRANGES];
+    int stride, resident, balanced;
+};
+static int launch_geo(raft_engine* e, StepKernel kern, int k, LaunchGeo& geo) {
+    const size_t lds = step_lds_bytes(k);
+    if (kern != (StepKernel)e->occ_kern || lds != e->occ_lds) {
+        int wg = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wg, (const void*)kern, STEP_BLOCK, lds));
+        e->occ_kern = (const void*)kern;
+        e->occ_lds = lds;
+        e->occ_wg = std::max(1, wg);
+    }
+    geo.resident = e->occ_wg * e->ncu;
+    const int cap = std::max(1, (e->sched_wg > 0 ? std::min(e->sched_wg, geo.resident) : geo.resident) / e->nsub);
+    geo.stride = 0;
+    geo.balanced = 0;
+    for (int q = 0; q < e->nsub; ++q) {
+        const int a = e->sub_b0[q] * STEP_WAVES, b = std::min(e->sub_b0[q + 1] * STEP_WAVES, e->nwaves);
+        const int n = b - a;
+        // AUTO: when the chunks outnumber the resident wave slots (of this
+        // sub-range's share); BALANCED: whenever a workgroup gets 4 chunks
+        const bool bal = e->schedule == RAFT_SCHED_BALANCED ? n >= STEP_WAVES
+                                                            : e->schedule == RAFT_SCHED_AUTO && n > STEP_WAVES * cap;
+        geo.w0[q] = a;
+        geo.w0[q + 1] = b;
+        geo.bal[q] = bal ? n : 0;
+        geo.nb[q] = bal ? std::min(cap, n / STEP_WAVES) : e->sub_b0[q + 1] - e->sub_b0[q];
+        geo.col0[q] = geo.stride;
+        geo.stride += geo.nb[q];
+        geo.balanced += bal;
+    }
+    return RAFT_OK;
+}
+
+template <int R> struct StepL {
+    static void run(raft_engine* e, StepKernel kern, uint32_t t0, int k, hipEvent_t ev0, hipEvent_t ev1,
+                    hipStream_t st, const LaunchGeo& geo, int q, uint32_t* partials) {
         // the launch's own start / stop timestamps (ev0, ev1 nullable): no
         // marker packets around the dispatch
         DevParams d = e->dp;
         d.part = partials;
-        d.wave0 = b0 * STEP_WAVES;
-        d.part_col0 = b0;
-        d.part_stride = e->nblocks;
-        hipExtLaunchKernelGGL(kern, dim3(b1 - b0), dim3(STEP_BLOCK), (uint32_t)lds, st, ev0, ev1, 0u, d, t0, k);
+        d.wave0 = geo.w0[q];
+        d.bal_chunks = geo.bal[q];
+        d.bal_q = geo.bal[q] / geo.nb[q];
+        d.bal_rem = geo.bal[q] % geo.nb[q];
+        d.part_col0 = geo.col0[q];
+        d.part_stride = geo.stride;
+        hipExtLaunchKernelGGL(kern, dim3(geo.nb[q]), dim3(STEP_BLOCK), (uint32_t)step_lds_bytes(k), st, ev0, ev1, 0u, d,
+                              t0, k);
     }
 };
 template <int R> struct PackL {
@@ -873,6 +1069,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_EINVAL, "ae_max_entries must be 0..RAFT_MAX_AE_ENTRIES, and 0 or 1 in reference mode");
     if (p->subranges < 0 || p->subranges > RAFT_MAX_SUBRANGES)
         return fail(RAFT_EINVAL, "subranges must be 0..RAFT_MAX_SUBRANGES");
+    if (p->schedule < RAFT_SCHED_AUTO || p->schedule > RAFT_SCHED_BALANCED || p->schedule_workgroups < 0)
+        return fail(RAFT_EINVAL, "schedule must be a RAFT_SCHED_* value and schedule_workgroups >= 0");
     if ((p->log_window ? p->log_window : p->log_cap) >= (1 << 23))
         return fail(RAFT_EINVAL, "log slots per replica (log_window, else log_cap) must be < 2^23");
     int ndev = 0;
@@ -890,6 +1088,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->launches_issued = 0;
     e->fork_needed = true;
     e->ev_fork = nullptr;
+    e->ev_wait = nullptr;
     for (int q = 0; q < RAFT_MAX_SUBRANGES; ++q) { e->sub_stream[q] = nullptr; e->ev_sub_done[q] = nullptr; }
     e->ev_red_done[0] = e->ev_red_done[1] = nullptr;
     e->bst = e->bio = e->hst = nullptr;
@@ -921,8 +1120,17 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.churn_steps = p->churn_steps; d.part_period = p->partition_period; d.part_len = p->partition_len;
     d.cmd_mode = p->cmd_mode; d.cmd_limit = p->cmd_limit;
     d.ae_max = p->mode == RAFT_MODE_TEXTBOOK && p->ae_max_entries > 1 ? p->ae_max_entries : 1;
-    const int64_t gpb = (int64_t)STEP_WAVES * (64 / p->R);          // groups per step workgroup
-    e->nblocks = (int)((G + gpb - 1) / gpb);
+    e->nwaves = (int)log_waves;
+    e->nblocks = (e->nwaves + STEP_WAVES - 1) / STEP_WAVES;
+    e->schedule = p->schedule;
+    e->sched_wg = p->schedule_workgroups;
+    e->occ_kern = nullptr;
+    e->occ_lds = 0;
+    e->occ_wg = 1;
+    e->last = raft_kernel_info{};
+    e->ncu = 0;
+    if (hipDeviceGetAttribute(&e->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || e->ncu < 1)
+        e->ncu = 1;
     d.GR = G * R;
     e->K = p->steps_per_launch > 0 ? p->steps_per_launch : 1;
 
@@ -935,7 +1143,6 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     // sized for the largest launch, so steps_per_launch can change later
     const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;
     const size_t cnt_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * RAFT_COUNTER_STRIDE * 8;
-    e->nchunks = (e->nblocks + REDUCE_CHUNK - 1) / REDUCE_CHUNK;
     const size_t acc_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NC * 8;
     e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + 2 * al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -1005,7 +1212,7 @@ int raft_engine_destroy(raft_engine* e) {
         if (e->sub_stream[q]) (void)hipStreamDestroy(e->sub_stream[q]);
         if (e->ev_sub_done[q]) (void)hipEventDestroy(e->ev_sub_done[q]);
     }
-    for (hipEvent_t x : {e->ev_fork, e->ev_red_done[0], e->ev_red_done[1]})
+    for (hipEvent_t x : {e->ev_fork, e->ev_red_done[0], e->ev_red_done[1], e->ev_wait})
         if (x) (void)hipEventDestroy(x);
     if (e->bst) (void)hipFree(e->bst);
     if (e->bio) (void)hipFree(e->bio);
@@ -1059,10 +1266,13 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
         for (int q = 0; q < e->nsub; ++q) HIP_TRY(hipStreamWaitEvent(e->sub_stream[q], e->ev_fork, 0));
         e->fork_needed = false;
     }
+    const StepKernel kern = n_steps > 0 ? step_kernel_of(e) : nullptr;
     for (int32_t done = 0; done < n_steps;) {
         const int k = std::min<int32_t>(e->K, n_steps - done);
         const int buf = split ? (int)(e->launches_issued & 1) : 0;
         uint32_t* part = buf ? e->partials2 : e->partials;
+        LaunchGeo geo;
+        if (int rc = launch_geo(e, kern, k, geo)) return rc;
         if (e->timing && e->ev_used + 2 * e->nsub > e->ev.size())
             if (int rc = reserve_events(e, 64 + e->nsub)) return rc;
         for (int q = 0; q < e->nsub; ++q) {
@@ -1074,17 +1284,25 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
             }
             hipStream_t st = split ? e->sub_stream[q] : e->stream;
             if (split && e->launches_issued >= 2) HIP_TRY(hipStreamWaitEvent(st, e->ev_red_done[buf], 0));
-            dispatch_R<StepL>(e->p.R, e, (uint32_t)(e->t + done), k, ev0, ev1, st, e->sub_b0[q], e->sub_b0[q + 1],
-                              part);
+            dispatch_R<StepL>(e->p.R, e, kern, (uint32_t)(e->t + done), k, ev0, ev1, st, geo, q, part);
             if (split) {
                 HIP_TRY(hipEventRecord(e->ev_sub_done[q], st));
                 HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_sub_done[q], 0));
             }
         }
         if (e->timing) ++e->timed_launches;
+        e->last = raft_kernel_info{};
+        e->last.net = step_net(e->dp, e->p, e->p.R, e->dp.churn_thr32 != 0 || e->iso_written);
+        e->last.textbook = e->p.mode == RAFT_MODE_TEXTBOOK;
+        e->last.ring = e->p.log_window != 0;
+        e->last.steps = k;
+        e->last.workgroups = geo.stride;
+        e->last.resident_workgroups = geo.resident;
+        e->last.balanced = geo.balanced;
+        e->last.subranges = e->nsub;
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
-        const dim3 rg((unsigned)e->nchunks, (unsigned)(k * NCW));
-        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(part, e->nblocks, e->p.R, dst, e->accum);
+        const dim3 rg((unsigned)((geo.stride + REDUCE_CHUNK - 1) / REDUCE_CHUNK), (unsigned)(k * NCW));
+        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(part, geo.stride, e->p.R, dst, e->accum);
         if (split) HIP_TRY(hipEventRecord(e->ev_red_done[buf], e->stream));
         ++e->launches_issued;
         done += k;
@@ -1141,18 +1359,23 @@ int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches)
         HIP_TRY(hipEventElapsedTime(&b, e->ev[0], e->ev[q + 1]));
         iv.emplace_back(a, b);
     }
+    // (an interval may start before ev[0]: a sub-range can run a launch ahead
+    // of sub-range 0, so the merge starts from the earliest interval)
     std::sort(iv.begin(), iv.end());
-    double acc = 0.0, lo = 0.0, hi = -1.0;
-    for (const auto& x : iv) {
-        if (x.first > hi) {
-            if (hi > lo) acc += hi - lo;
-            lo = x.first;
-            hi = x.second;
-        } else {
-            hi = std::max(hi, x.second);
+    double acc = 0.0;
+    if (!iv.empty()) {
+        double lo = iv[0].first, hi = iv[0].second;
+        for (size_t q = 1; q < iv.size(); ++q) {
+            if (iv[q].first > hi) {
+                acc += hi - lo;
+                lo = iv[q].first;
+                hi = iv[q].second;
+            } else {
+                hi = std::max(hi, iv[q].second);
+            }
         }
+        acc += hi - lo;
     }
-    if (hi > lo) acc += hi - lo;
     *total_ms = acc;
     *launches = e->timed_launches;
     e->ev_used = 0;
@@ -1167,11 +1390,25 @@ int raft_engine_set_steps_per_launch(raft_engine* e, int32_t k) {
     return RAFT_OK;
 }
 // Sub-ranges: contiguous workgroup ranges of (nearly) equal size.  Automatic
-// (n = 0): three ranges, the best measured at 1.25e5 .. 1e6 groups (config 3)
-// and for config 5 (1.25e5 groups 1.36 -> 1.73e10, 1e6 groups
-// 1.78 -> 1.86e10 group-steps/s); the engine stream plus three sub-range
-// streams stay within GPU_MAX_HW_QUEUES = 4 hardware queues.
-constexpr int AUTO_SUBRANGES = 3;
+// (n = 0): one.  (ABI 1 chose three, which overlapped one range's last waves
+// with another's next launch: 1.25e5 groups 1.36 -> 1.73e10, 1e6 groups 1.78
+// -> 1.86e10 group-steps/s; the balanced schedule ends a launch's waves
+// together instead, with no side streams)
+constexpr int AUTO_SUBRANGES = 1;
+int raft_engine_wait_stream(raft_engine* e, void* stream) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    if (!e->ev_wait) HIP_TRY(hipEventCreateWithFlags(&e->ev_wait, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(e->ev_wait, (hipStream_t)stream));
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_wait, 0));
+    e->fork_needed = true;                 // the sub-range streams must see it too
+    return RAFT_OK;
+}
+int raft_engine_kernel_info(raft_engine* e, raft_kernel_info* out) {
+    if (!e || !out) return fail(RAFT_EINVAL, "null argument");
+    *out = e->last;
+    return RAFT_OK;
+}
 int raft_engine_set_subranges(raft_engine* e, int32_t n) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     if (n < 0 || n > RAFT_MAX_SUBRANGES) return fail(RAFT_EINVAL, "subranges must be 0..RAFT_MAX_SUBRANGES");

@@ -118,10 +118,14 @@ struct DevParams {
     int32_t cmd_mode, cmd_limit;
     int32_t ae_max;                            // entries per AppendEntries request (textbook mode; else 1)
     uint32_t rk[20];                           // Philox round keys (k0, k1) of rounds 0..9 (kdraw)
-    // step_kernel launches only: this launch's sub-range of the waves and its
-    // columns of the counter partials [k][NCW][part_stride]
+    // step_kernel launches only: this launch's sub-range of the waves (chunks
+    // of GPW groups, one log block each), its columns of the counter partials
+    // [k][NCW][part_stride], and its schedule: bal_chunks == 0, one chunk per
+    // wave (wave0 + blockIdx.x * STEP_WAVES + wave); else the balanced
+    // schedule over bal_chunks chunks (raft_engine.hip piece_of)
     uint32_t* part;
     int32_t wave0, part_col0, part_stride;
+    int32_t bal_chunks, bal_q, bal_rem;        // (bal_q, bal_rem) = bal_chunks / and % the workgroups
 };
 
 constexpr int32_t FLAT_W = 1 << 30;            // DevParams::W of a flat log (log_window 0): nothing is ever below it

@@ -91,6 +91,15 @@ class RaftEngine:
             return                                   # an older experimental build: one range
         self._check(self._lib.raft_engine_set_subranges(self._h, int(n)), "set_subranges")
 
+    def kernel_info(self) -> dict:
+        """The step kernel and schedule of the last step launch
+        (raft_engine_kernel_info): net (raft_step.h NET_* bits), textbook, ring,
+        steps, workgroups, resident_workgroups, balanced (sub-ranges on the
+        balanced schedule), subranges."""
+        k = abi.raft_kernel_info()
+        self._check(self._lib.raft_engine_kernel_info(self._h, C.byref(k)), "kernel_info")
+        return {n: int(getattr(k, n)) for n, _ in abi.raft_kernel_info._fields_ if n != "reserved"}
+
     @property
     def device_bytes(self) -> int:
         return int(self._lib.raft_engine_device_bytes(self._h))
@@ -233,18 +242,36 @@ class RaftEngine:
 
 
     # -- the same batches on device buffers (HBM-resident inputs) ------------
-    def vote_batch_dev(self, group_ptr: int, dst_ptr: int, req_ptr: int, resp_ptr: int, n: int):
+    # The engine stream does not wait for other streams: the buffers must be
+    # complete before the call.  `after_stream` (a hipStream_t handle, e.g.
+    # torch.cuda.current_stream().cuda_stream) orders the batch after all work
+    # enqueued on that stream so far (raft_engine_wait_stream).
+    def wait_stream(self, stream: int | None):
+        """Order the engine stream after all work enqueued so far on `stream`
+        (None / 0: the null stream)."""
+        self._check(self._lib.raft_engine_wait_stream(self._h, C.c_void_p(stream or 0)), "wait_stream")
+
+    def vote_batch_dev(self, group_ptr: int, dst_ptr: int, req_ptr: int, resp_ptr: int, n: int,
+                       after_stream: int | None = None):
         """raft_vote_batch_dev: DEVICE pointers to n int64 groups, int32
         replicas, raft_vote_req and raft_vote_resp (e.g. torch tensors'
         data_ptr() on this engine's GPU)."""
+        if after_stream is not None:
+            self.wait_stream(after_stream)
         self._check(self._lib.raft_vote_batch_dev(self._h, group_ptr, dst_ptr, req_ptr, resp_ptr, int(n)),
                     "raft_vote_batch_dev")
 
-    def append_batch_dev(self, group_ptr: int, dst_ptr: int, req_ptr: int, resp_ptr: int, n: int):
+    def append_batch_dev(self, group_ptr: int, dst_ptr: int, req_ptr: int, resp_ptr: int, n: int,
+                         after_stream: int | None = None):
+        if after_stream is not None:
+            self.wait_stream(after_stream)
         self._check(self._lib.raft_append_batch_dev(self._h, group_ptr, dst_ptr, req_ptr, resp_ptr, int(n)),
                     "raft_append_batch_dev")
 
-    def append_command_batch_dev(self, group_ptr: int, replica_ptr: int, cmd_ptr: int, n: int):
+    def append_command_batch_dev(self, group_ptr: int, replica_ptr: int, cmd_ptr: int, n: int,
+                                 after_stream: int | None = None):
+        if after_stream is not None:
+            self.wait_stream(after_stream)
         self._check(self._lib.raft_append_command_batch_dev(self._h, group_ptr, replica_ptr, cmd_ptr, int(n)),
                     "raft_append_command_batch_dev")
 

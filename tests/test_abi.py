@@ -46,7 +46,7 @@ def test_library_is_gfx950(lib):
 
 
 def test_abi_version_and_defaults(lib):
-    assert lib.raft_abi_version() == 1
+    assert lib.raft_abi_version() == 2
     p = abi.raft_params()
     lib.raft_params_default(C.byref(p))
     for k, v in abi.DEFAULTS.items():

@@ -50,29 +50,39 @@ def test_timed_launches_have_one_length(steps, spl, want):
         assert set(bench.launch_plan(steps, L)) == {L}
 
 
-def test_gpus_2_spawns_two_gloo_ranks():
-    """Weak scaling by default (the path shards with no exchange): every rank
-    its own 10^6 groups, in contiguous global-id ranges."""
+def test_gpus_2_spawns_two_gloo_ranks_config4_by_default():
+    """Config 4 (BASELINE.json configs[3]) by default: the 10^6 groups split
+    into contiguous global-id ranges over the ranks (strong scaling)."""
     r = run(["--gpus", "2", "--plan-only"])
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout                      # rank 0 prints the one line
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
-    assert out["shards"] == [[0, 0, 1_000_000], [1, 1_000_000, 1_000_000]]
-
-
-def test_gpus_2_strong_shards_config4():
-    r = run(["--gpus", "2", "--plan-only", "--scaling", "strong"])
-    assert r.returncode == 0, r.stderr[-2000:]
-    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert out["scaling"] == "strong"
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
     assert out["shards"] == [[0, 0, 500_000], [1, 500_000, 500_000]]
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_gpus_n_strong_shards_config4(world):
+    r = run(["--gpus", str(world), "--plan-only"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    per = 1_000_000 // world
+    assert out["scaling"] == "strong" and out["shards"] == [[q, q * per, per] for q in range(world)]
+
+
+def test_gpus_2_weak_shards_on_request():
+    r = run(["--gpus", "2", "--plan-only", "--scaling", "weak"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["scaling"] == "weak"
+    assert out["shards"] == [[0, 0, 1_000_000], [1, 1_000_000, 1_000_000]]
+
+
 def test_rank0_weak_shard_is_the_strong_leg_groups():
-    """The config-4 leg of a weak job splits groups 0..G-1 over the ranks; rank
-    0's weak shard is exactly those global groups, so their counters agree."""
+    """The strong (config 4) leg splits groups 0..G-1 over the ranks; rank 0's
+    weak shard (the side leg) is exactly those global groups, so rank 0's weak
+    rows equal the strong leg's all-reduced rows."""
     for world in (2, 4, 8):
         g0, n = bench.shard(1_000_000, world, 0, "weak")
         strong = [bench.shard(1_000_000, world, r, "strong") for r in range(world)]

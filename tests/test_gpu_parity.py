@@ -250,6 +250,90 @@ def test_subrange_invariance():
     assert (e.digest(), np.concatenate([c1, c2, c3]).tobytes()) == ref
 
 
+@pytest.fixture(scope="module")
+def oracle_runs():
+    """Oracle runs shared by the schedule tests: {name: (params kw, steps, counters, digest)}."""
+    out = {}
+    for name, kw, steps, cap in (
+            ("c3", dict(abi.CONFIGS[3], G=4000, churn_ppm=10_000), 300, 200),
+            ("c5", dict(abi.CONFIGS[5], G=2000), 300, 400),
+            ("c2", dict(abi.CONFIGS[2], G=3000), 200, 200)):
+        o = O.Oracle(abi.make_params(log_cap=cap, **kw))
+        co = o.step(steps, nthreads=NTHREADS)[:, : abi.NUM_COUNTERS]
+        out[name] = (dict(kw, log_cap=cap), steps, co, o.digest())
+        o.close()
+    return out
+
+
+# (workgroups, steps per launch, sub-ranges): at G = 4000 x 5 there are 334
+# chunks (64 // R groups each), so 1 workgroup takes all of them (each wave a
+# quarter of 334 x K chunk-steps), 7 about 48 (heads and tails of every
+# length), 83 four or five (the smallest split)
+BALANCED_CASES = [(1, 20, 1), (3, 7, 1), (7, 37, 1), (7, 400, 1), (50, 20, 1), (83, 20, 1), (83, 1, 1),
+                  (7, 64, 2), (40, 400, 3)]
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c5", "c2"])
+@pytest.mark.parametrize("case", BALANCED_CASES, ids=[f"wg{a}-k{b}-sub{c}" for a, b, c in BALANCED_CASES])
+def test_balanced_schedule_vs_oracle(oracle_runs, cfg, case):
+    """The balanced schedule (raft_params.schedule): a
+    workgroup's waves split its chunks' chunk-steps, a chunk passing from one
+    wave to the next between two steps through HBM and an in-workgroup LDS
+    flag.  Every per-step counter and the whole-run digest equal the oracle's
+    (configs 3, 5 and 2 at reduced G: drops and churn, partitions -- redrawn at
+    a piece's first step --, and R = 3)."""
+    nwg, spl, nsub = case
+    kw, steps, co, dg = oracle_runs[cfg]
+    e = RaftEngine(abi.make_params(steps_per_launch=spl, subranges=nsub, schedule=abi.SCHED_BALANCED,
+                                   schedule_workgroups=nwg, **kw))
+    try:
+        ce = e.step(steps)
+        info = e.kernel_info()
+        assert info["balanced"] == nsub and info["subranges"] == nsub
+        assert info["workgroups"] <= nwg
+        if not np.array_equal(ce, co):
+            bad = np.argwhere(ce != co)[0]
+            raise AssertionError(f"{cfg} {case}: counters differ at step {bad[0]} ({abi.COUNTER_NAMES[bad[1]]})")
+        assert e.digest() == dg
+    finally:
+        e.close()
+
+
+def test_one_per_wave_schedule_vs_oracle(oracle_runs):
+    """The one-chunk-per-wave schedule, forced (RAFT_SCHED_ONE_PER_WAVE), on the same runs."""
+    for cfg in ("c3", "c5", "c2"):
+        kw, steps, co, dg = oracle_runs[cfg]
+        e = RaftEngine(abi.make_params(steps_per_launch=37, schedule=abi.SCHED_ONE_PER_WAVE, **kw))
+        ce = e.step(steps)
+        assert e.kernel_info()["balanced"] == 0
+        assert np.array_equal(ce, co) and e.digest() == dg, cfg
+        e.close()
+
+
+def test_kernel_info_names_the_launched_kernel():
+    """raft_engine_kernel_info reports the NET variant the engine launched,
+    which must be the one abi.step_net predicts (bench.py's launch lengths and
+    occupancy assumptions rest on it), including an engine that would get the
+    partitions-only kernel until write_state stores an isolation word."""
+    cases = [dict(abi.CONFIGS[3], G=600), dict(abi.CONFIGS[5], G=600), dict(abi.CONFIGS[2], G=600),
+             dict(abi.CONFIGS[3], G=600, partition_period=40, partition_len=10), dict(R=4, G=600, drop_ppm=1000)]
+    for kw in cases:
+        e = RaftEngine(abi.make_params(log_cap=64, **kw))
+        e.step(1)
+        assert e.kernel_info()["net"] == abi.step_net_of(kw), kw
+        e.close()
+    kw = dict(abi.CONFIGS[2], G=600)
+    e = RaftEngine(abi.make_params(log_cap=64, **kw))
+    e.step(1)
+    assert e.kernel_info()["net"] == abi.NET_PART
+    st = e.read_state()
+    st[0, -2] = (3 << 8) | 1                              # replica 1 isolated for 3 steps
+    e.write_state(st)
+    e.step(1)
+    assert e.kernel_info()["net"] == abi.step_net(3, iso_written=True) == abi.NET_ALL
+    e.close()
+
+
 def test_shard_invariance():
     """Config 4's contract: sharding by global group id does not change any group."""
     kw = dict(abi.CONFIGS[3])
@@ -365,17 +449,24 @@ FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_
 # it at 6 workgroups per CU).
 # A fourth element is the launch sub-ranges (streams); default: the engine's
 # automatic choice (3, the bench's configuration).
+# A fourth element is the launch sub-ranges (streams; default 1, the engine's
+# automatic choice), a fifth the schedule (default automatic: balanced
+# whenever the chunks outnumber the resident wave slots, which they do at
+# both full sizes).  (3, 0, 20, 1) is the driver's exact timed launch.
+ONE = abi.SCHED_ONE_PER_WAVE
 FULL_SIZE_CASES = [
-    (3, 0, 1), (3, 0, 20), (3, 0, abi.BENCH_STEPS_PER_LAUNCH), (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 1),
+    (3, 0, 1), (3, 0, 20, 1), (3, 0, 20, 1, ONE), (3, 0, abi.BENCH_STEPS_PER_LAUNCH),
+    (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3, ONE),
     (3, 256, 1), (3, 256, abi.BENCH_STEPS_PER_LAUNCH), (3, 256, abi.MAX_STEPS_PER_LAUNCH),
     (5, 0, 1), (5, 0, abi.BENCH_STEPS_PER_LAUNCH), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH),
-    (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 1), (5, 0, 500, 4),
+    (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (5, 0, 500, 4, ONE),
 ]
 
 
 def _full_id(case):
     c, w, k = case[:3]
-    return f"{c}-{'flat' if w == 0 else f'ring{w}'}-{k}" + (f"-sub{case[3]}" if len(case) > 3 else "")
+    return (f"{c}-{'flat' if w == 0 else f'ring{w}'}-{k}" + (f"-sub{case[3]}" if len(case) > 3 else "")
+            + ("-onewave" if len(case) > 4 and case[4] == ONE else ""))
 
 
 @pytest.mark.parametrize("case", FULL_SIZE_CASES, ids=[_full_id(c) for c in FULL_SIZE_CASES])
@@ -392,14 +483,16 @@ def test_full_size_digest(case):
     import json
     cfg, window, spl = case[:3]
     nsub = case[3] if len(case) > 3 else 0
+    sched = case[4] if len(case) > 4 else abi.SCHED_AUTO
     meta = json.load(open(FULL))[f"c{cfg}"]
     want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))[f"c{cfg}_counters"]
     kw = dict(abi.CONFIGS[cfg])
     assert meta["groups"] == kw["G"] and meta["params"] == {k: v for k, v in kw.items() if k != "G"}
     e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], log_window=window, steps_per_launch=spl,
-                                   subranges=nsub, **kw))
+                                   subranges=nsub, schedule=sched, **kw))
     try:
         ce = e.step(meta["steps"])
+        assert e.kernel_info()["balanced"] == (0 if sched == ONE else e.subranges)
         if not np.array_equal(ce, want):
             bad = np.argwhere(ce != want)[0]
             raise AssertionError(f"config {cfg}: counters differ at step {bad[0]} ({abi.COUNTER_NAMES[bad[1]]}): "
@@ -412,6 +505,41 @@ def test_full_size_digest(case):
         assert ce[:, abi.C_INDEX["log_window_miss"]].sum() == 0
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_config4_strong_split_full_size(n):
+    """BASELINE config 4 at full size on one GPU: config 3's 10^6 x 5 groups
+    split into n contiguous global-id shards (bench.shard, "strong": the
+    ranks of `bench.py --gpus n`), each its own engine at its global offset
+    g0, created and closed in turn, for 10^4 steps -- at the driver's launch
+    (20 steps, one sub-range) and at the bench default (400).  The summed
+    per-step counter rows equal the oracle's for the whole 10^6 groups
+    (full_size_counters.npz) and the digests sum (mod 2^64) to its whole-run
+    digest over every physical slot (the digest is a sum over groups)."""
+    import json
+    import bench
+    meta = json.load(open(FULL))["c3"]
+    want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))["c3_counters"]
+    kw = dict(abi.CONFIGS[3])
+    for spl in (20, abi.BENCH_STEPS_PER_LAUNCH):
+        total = np.zeros_like(want)
+        dsum = 0
+        for rank in range(n):
+            g0, G = bench.shard(kw["G"], n, rank, "strong")
+            e = RaftEngine(abi.make_params(log_cap=meta["log_cap"], steps_per_launch=spl, subranges=1,
+                                           **dict(kw, G=G, g0=g0)))
+            try:
+                total += e.step(meta["steps"])
+                dsum = (dsum + e.digest()) % (1 << 64)
+                assert e.kernel_info()["balanced"] == 1          # every shard outnumbers the wave slots
+            finally:
+                e.close()
+        if not np.array_equal(total, want):
+            bad = np.argwhere(total != want)[0]
+            raise AssertionError(f"{n} shards, K = {spl}: counters differ at step {bad[0]} "
+                                 f"({abi.COUNTER_NAMES[bad[1]]}): {total[tuple(bad)]} vs {want[tuple(bad)]}")
+        assert f"{dsum:016x}" == meta["digest_full_log"], f"{n} shards, K = {spl}: digest sum differs"
 
 
 def test_full_size_config3_1e5_steps_on_the_ring():
@@ -582,19 +710,21 @@ def test_device_batches_match_host_batches():
                    rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)], axis=1).astype(np.int64)
     cmd = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     dev = torch.device("cuda", 0)
+    cur = lambda: torch.cuda.current_stream(dev).cuda_stream  # noqa: E731
     tg, td = torch.from_numpy(grp.astype(np.int64)).to(dev), torch.from_numpy(dst).to(dev)
     ve = a.vote_batch(grp, dst, vq)
     tv, tvr = torch.from_numpy(vq).to(dev), torch.zeros((n, 2), dtype=torch.int32, device=dev)
-    b.vote_batch_dev(tg.data_ptr(), td.data_ptr(), tv.data_ptr(), tvr.data_ptr(), n)
+    # the inputs and the zeroed responses come from torch's stream: order the batch after it
+    b.vote_batch_dev(tg.data_ptr(), td.data_ptr(), tv.data_ptr(), tvr.data_ptr(), n, after_stream=cur())
     assert np.array_equal(ve, tvr.cpu().numpy())
     ae = a.append_batch(grp, dst, aq)
     ta = torch.from_numpy(aq.astype(np.uint32).view(np.int32)).to(dev)
     tar = torch.zeros((n, 3), dtype=torch.int32, device=dev)
-    b.append_batch_dev(tg.data_ptr(), td.data_ptr(), ta.data_ptr(), tar.data_ptr(), n)
+    b.append_batch_dev(tg.data_ptr(), td.data_ptr(), ta.data_ptr(), tar.data_ptr(), n, after_stream=cur())
     assert np.array_equal(ae, tar.cpu().numpy())
     a.append_command_batch(grp, dst, cmd)
     tc = torch.from_numpy(cmd.view(np.int32)).to(dev)
-    b.append_command_batch_dev(tg.data_ptr(), td.data_ptr(), tc.data_ptr(), n)
+    b.append_command_batch_dev(tg.data_ptr(), td.data_ptr(), tc.data_ptr(), n, after_stream=cur())
     sa = a.read_state()
     assert np.array_equal(sa, b.read_state())
     assert_same_logs(sa, a.read_log(), b.read_log(), R, "device vs host batches")
