@@ -59,6 +59,12 @@ KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h")
 SCHEDULES = {"auto": abi.SCHED_AUTO, "one": abi.SCHED_ONE_PER_WAVE, "balanced": abi.SCHED_BALANCED}
 
 
+def NET_NAMES(net: int) -> list:
+    """The network faults / harness a step kernel is built for (raft_step.h NET_*)."""
+    return [n for b, n in ((abi.NET_DROP, "drops"), (abi.NET_PART, "partitions"), (abi.NET_ISO, "isolation_churn"),
+                           (abi.NET_CMDLOW, "commands_to_lowest_leader_compiled_in")) if net & b]
+
+
 def kernel_source_id() -> str:
     """Short hash of the step kernel's sources: a PMC row describes one kernel
     build, so bench.py attaches it only to a run of the same sources."""
@@ -275,6 +281,8 @@ def parse_args(argv=None):
     ap.add_argument("--reduce-every", type=int, default=512,
                     help="steps per counter all-reduce (rounded to whole launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-general-leg", action="store_true",
+                    help="N = 1: skip the general_kernel leg (the main leg on the run-time-decided kernel)")
     ap.add_argument("--handler-batch", type=int, default=1_000_000,
                     help="messages per single-handler batch of the handler_batch leg (0 = skip the leg)")
     ap.add_argument("--handler-reps", type=int, default=20)
@@ -611,6 +619,31 @@ def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, s
     return out
 
 
+def general_kernel_leg(eng, args, chunk, dev, main_rows, main_kern_avg_ms):
+    """The main leg again on the same engine (reset to step 0) with the
+    general step kernel, which decides every network fault and the command
+    harness at run time (raft_params.kernel = RAFT_KERNEL_GENERAL), where the
+    main leg ran the kernel built for the workload (config 3: drops and churn,
+    no partitions, commands to the lowest LEADER compiled in).  Same warmup,
+    steps and launches; its counter rows must equal the main leg's."""
+    eng.set_kernel(abi.KERNEL_GENERAL)
+    eng.reset()
+    try:
+        leg = timed_leg(eng, args, chunk, False, dev, 1)
+        info = eng.kernel_info()
+    finally:
+        eng.set_kernel(abi.KERNEL_AUTO)
+    rows = leg["counters"].cpu().numpy()[:, : abi.NUM_COUNTERS]
+    return {"value": eng.G * args.steps / leg["elapsed"], "unit": "group-steps/s",
+            "kernel_net": info["net"], "kernel_avg_ms": leg["kern_avg_ms"],
+            "kernel_time_vs_specialised": leg["kern_avg_ms"] / main_kern_avg_ms if main_kern_avg_ms else None,
+            "counters_equal_main_leg": bool(np.array_equal(rows, main_rows)),
+            "note": "the same warmup, steps and launches on the same engine (reset to step 0) with the general "
+                    "step kernel (NET_ALL: drops, partitions and isolation churn decided at run time, the command "
+                    "harness read from the parameters); the main leg's kernel is built for the workload "
+                    "(roofline.kernel_variant)"}
+
+
 def plan_only(args, world, rank):
     """The rank/shard plumbing without a GPU (tests/test_bench_cpu.py)."""
     import torch
@@ -710,6 +743,10 @@ def main(argv=None, result=None):
     elapsed, kern_avg_ms, kern_avg_per_rank = leg["elapsed"], leg["kern_avg_ms"], leg["kern_avg_per_rank"]
     counters, gcounters, wcount = leg["counters"], leg["gcounters"], leg["wcount"]
 
+    kinfo = eng.kernel_info()                                # the timed leg's last launch
+    kernel_variant = {"net": kinfo["net"], "net_bits": NET_NAMES(kinfo["net"]), "textbook": bool(kinfo["textbook"]),
+                      "ring": bool(kinfo["ring"]), "schedule": "balanced" if kinfo["balanced"] else "one_per_wave",
+                      "workgroups": kinfo["workgroups"], "resident_workgroups": kinfo["resident_workgroups"]}
     c_all = gcounters.cpu().numpy()[:, : abi.NUM_COUNTERS]    # all ranks' groups
     c_loc = counters.cpu().numpy()[:, : abi.NUM_COUNTERS]     # this rank's groups (before the all-reduce)
     value = total_groups * args.steps / elapsed
@@ -786,6 +823,10 @@ def main(argv=None, result=None):
                      "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
+    general = None
+    if world == 1 and not coll and not args.no_general_leg and net != abi.NET_ALL:
+        general = general_kernel_leg(eng, args, chunk, dev, c_loc, kern_avg_ms)
+
     if args.plan_file and rank == 0:
         # [leg, steps, dispatches]: a launch of the warmup / timed legs is one
         # step-kernel dispatch per sub-range; the streaming leg runs one range
@@ -860,6 +901,7 @@ def main(argv=None, result=None):
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_frac": traffic / (kern_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None,
             "kernel": f"step_kernel<{R}> x{L} fused steps", "launch_steps": L,
+            "kernel_variant": kernel_variant,
             "kernel_avg_ms": kern_avg_ms, "kernel_avg_ms_per_rank": kern_avg_per_rank, "launches": launches,
             "alg_bytes_per_launch": bytes_alg / max(1, launches),
             "alg_bytes_per_group_step": bytes_alg / max(1, G_local * c_loc.shape[0]),
@@ -875,6 +917,7 @@ def main(argv=None, result=None):
                     "binding roofline. roofline_streaming is the same step at one step per launch",
         },
         "roofline_valu": roofline_valu,
+        "general_kernel": general,
         "roofline_streaming": streaming,
         "timing": {"wall_ms": wall * 1e3, "stream_event_ms": ev_ms, "step_kernel_ms_total": kern_ms,
                    "note": "the timed region: each rank's wall clock from after the opening barrier + device "

@@ -40,8 +40,9 @@
 extern "C" {
 #endif
 
-/* 2: raft_params.schedule / schedule_workgroups, automatic subranges = 1,
- * raft_engine_kernel_info */
+/* 2: raft_params.schedule / schedule_workgroups / kernel, automatic
+ * subranges = 1, raft_engine_kernel_info, raft_engine_set_kernel,
+ * raft_engine_reset, raft_engine_wait_stream */
 #define RAFT_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
@@ -105,7 +106,7 @@ typedef struct raft_params {
     int32_t  cmd_mode;          /* RAFT_CMD_*                                                       */
     int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
     int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch, 0..RAFT_MAX_STEPS_PER_LAUNCH (0 = 1);
-                                   results never depend on it; <= 433 lets the 7-wave kernels (R <= 5, and
+                                   results never depend on it; <= 431 lets the 7-wave kernels (R <= 5, and
                                    R = 7 without drops) run 7 workgroups per CU (LDS), longer launches run 6 */
     int32_t  mode;              /* RAFT_MODE_* (0 = the reference)                                  */
     int32_t  log_window;        /* 0 = every physical slot is kept (log_cap slots per replica);
@@ -130,8 +131,13 @@ typedef struct raft_params {
                                  * on it.                                                          */
     int32_t  schedule_workgroups; /* engine only: workgroups of a balanced launch (0 = as many as
                                  * the GPU holds at once at the launch's LDS; tests set fewer)     */
-    int32_t  reserved[1];
+    int32_t  kernel;            /* engine only: RAFT_KERNEL_AUTO (0): the step kernel built for the
+                                 * configured network faults and command harness (the other checks
+                                 * compiled out); RAFT_KERNEL_GENERAL: the kernel that decides every
+                                 * fault at run time.  Results never depend on it.                 */
 } raft_params;
+#define RAFT_KERNEL_AUTO    0
+#define RAFT_KERNEL_GENERAL 1
 
 /* ---- step-kernel schedules (raft_params.schedule) --------
  * A chunk is one wave's 64 / R groups.  ONE_PER_WAVE launches a wave per
@@ -286,6 +292,13 @@ int     raft_engine_set_subranges(raft_engine* e, int32_t n);
 int32_t raft_engine_subranges(raft_engine* e);    /* the sub-ranges in use (-1: null engine) */
 /* The step kernel and schedule of the last step launch (zeros before the first). */
 int     raft_engine_kernel_info(raft_engine* e, raft_kernel_info* out);
+/* The step kernel variant from now on (raft_params.kernel).  Results do not
+ * depend on it. */
+int     raft_engine_set_kernel(raft_engine* e, int32_t kernel);
+/* Every group back to the reference's initial state at step 0, exactly as
+ * raft_engine_create leaves it (RaftServer.kt:35-48, the election timers armed
+ * as init does, :58). */
+int     raft_engine_reset(raft_engine* e);
 /* Set the index of the next step (its Philox counter c0); with write_state
  * this resumes a run exported at any step. */
 int     raft_engine_set_step_index(raft_engine* e, int64_t t);

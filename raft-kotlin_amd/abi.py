@@ -47,7 +47,7 @@ MAX_STEPS_PER_LAUNCH = 512
 # bench.py's launch length for the step kernels built for 7 waves per SIMD
 # (R <= 5, or R = 7 without drops; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
 # the longest that keeps 7 step workgroups per CU within the LDS (STEP_K_7WG,
-# 433 steps).  The other kernels run 6 workgroups per CU at any length and
+# 431 steps).  The other kernels run 6 workgroups per CU at any length and
 # take the longest launch.
 BENCH_STEPS_PER_LAUNCH = 400
 
@@ -116,12 +116,14 @@ class raft_params(C.Structure):
         ("cmd_ppm", C.c_uint32), ("cmd_mode", C.c_int32), ("cmd_limit", C.c_int32),
         ("steps_per_launch", C.c_int32), ("mode", C.c_int32), ("log_window", C.c_int32),
         ("ae_max_entries", C.c_int32), ("subranges", C.c_int32), ("schedule", C.c_int32),
-        ("schedule_workgroups", C.c_int32), ("reserved", C.c_int32 * 1),
+        ("schedule_workgroups", C.c_int32), ("kernel", C.c_int32),
     ]
 
 
 # step-kernel schedules (raft_params.schedule)
 SCHED_AUTO, SCHED_ONE_PER_WAVE, SCHED_BALANCED = 0, 1, 2
+# step-kernel variant (raft_params.kernel): built for the workload, or the general one
+KERNEL_AUTO, KERNEL_GENERAL = 0, 1
 
 
 class raft_kernel_info(C.Structure):
@@ -244,6 +246,8 @@ def load_library(path: str | None = None):
         "raft_engine_subranges": (I32, [eng]),
         "raft_engine_kernel_info": (C.c_int, [eng, P(raft_kernel_info)]),
         "raft_engine_wait_stream": (C.c_int, [eng, C.c_void_p]),
+        "raft_engine_set_kernel": (C.c_int, [eng, I32]),
+        "raft_engine_reset": (C.c_int, [eng]),
         "raft_engine_device_bytes": (I64, [eng]),
         "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
         "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
@@ -294,6 +298,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
     "raft_engine_set_subranges", "raft_engine_subranges", "raft_engine_kernel_info", "raft_engine_wait_stream",
+    "raft_engine_set_kernel", "raft_engine_reset",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",

@@ -909,6 +909,7 @@ static int step_net(const DevParams& d, const raft_params& p, int R, bool iso) {
 }
 template <int R, bool TB, bool RING>
 static StepKernel step_fn(const DevParams& d, const raft_params& p, bool iso) {
+    if (p.kernel == RAFT_KERNEL_GENERAL) return step_kernel<R, TB, RING, NET_ALL>;
     if constexpr (R == 3 || R == 5 || R == 7) {
         const int net = step_net(d, p, R, iso);
         if (net == (NET_DROP | NET_ISO | NET_CMDLOW)) return step_kernel<R, TB, RING, NET_DROP | NET_ISO | NET_CMDLOW>;
@@ -1071,6 +1072,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         return fail(RAFT_EINVAL, "subranges must be 0..RAFT_MAX_SUBRANGES");
     if (p->schedule < RAFT_SCHED_AUTO || p->schedule > RAFT_SCHED_BALANCED || p->schedule_workgroups < 0)
         return fail(RAFT_EINVAL, "schedule must be a RAFT_SCHED_* value and schedule_workgroups >= 0");
+    if (p->kernel != RAFT_KERNEL_AUTO && p->kernel != RAFT_KERNEL_GENERAL)
+        return fail(RAFT_EINVAL, "kernel must be RAFT_KERNEL_AUTO or RAFT_KERNEL_GENERAL");
     if ((p->log_window ? p->log_window : p->log_cap) >= (1 << 23))
         return fail(RAFT_EINVAL, "log slots per replica (log_window, else log_cap) must be < 2^23");
     int ndev = 0;
@@ -1292,7 +1295,8 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
         }
         if (e->timing) ++e->timed_launches;
         e->last = raft_kernel_info{};
-        e->last.net = step_net(e->dp, e->p, e->p.R, e->dp.churn_thr32 != 0 || e->iso_written);
+        e->last.net = e->p.kernel == RAFT_KERNEL_GENERAL
+                          ? NET_ALL : step_net(e->dp, e->p, e->p.R, e->dp.churn_thr32 != 0 || e->iso_written);
         e->last.textbook = e->p.mode == RAFT_MODE_TEXTBOOK;
         e->last.ring = e->p.log_window != 0;
         e->last.steps = k;
@@ -1402,6 +1406,27 @@ int raft_engine_wait_stream(raft_engine* e, void* stream) {
     HIP_TRY(hipEventRecord(e->ev_wait, (hipStream_t)stream));
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_wait, 0));
     e->fork_needed = true;                 // the sub-range streams must see it too
+    return RAFT_OK;
+}
+int raft_engine_set_kernel(raft_engine* e, int32_t kernel) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (kernel != RAFT_KERNEL_AUTO && kernel != RAFT_KERNEL_GENERAL)
+        return fail(RAFT_EINVAL, "kernel must be RAFT_KERNEL_AUTO or RAFT_KERNEL_GENERAL");
+    e->p.kernel = kernel;
+    return RAFT_OK;
+}
+int raft_engine_reset(raft_engine* e) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int q = 0; q < e->nsub && e->nsub > 1; ++q) HIP_TRY(hipStreamSynchronize(e->sub_stream[q]));
+    dispatch_R<InitL>(e->p.R, e);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->t = 0;
+    e->cache_valid = true;                 // init zeroes the tail cache with the logs' lastIndex
+    e->iso_written = false;
+    e->fork_needed = true;
     return RAFT_OK;
 }
 int raft_engine_kernel_info(raft_engine* e, raft_kernel_info* out) {

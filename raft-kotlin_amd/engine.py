@@ -91,6 +91,15 @@ class RaftEngine:
             return                                   # an older experimental build: one range
         self._check(self._lib.raft_engine_set_subranges(self._h, int(n)), "set_subranges")
 
+    def set_kernel(self, kernel: int):
+        """The step kernel variant from now on (abi.KERNEL_AUTO / KERNEL_GENERAL;
+        results do not depend on it)."""
+        self._check(self._lib.raft_engine_set_kernel(self._h, int(kernel)), "set_kernel")
+
+    def reset(self):
+        """Every group back to its initial state at step 0 (as created)."""
+        self._check(self._lib.raft_engine_reset(self._h), "reset")
+
     def kernel_info(self) -> dict:
         """The step kernel and schedule of the last step launch
         (raft_engine_kernel_info): net (raft_step.h NET_* bits), textbook, ring,

@@ -9,7 +9,7 @@ step() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.
          echo "$name rc=$rc" >> "$OUT/status.txt"; [ $rc -eq 0 ] || [ $rc -eq 1 -a "$name" = pytest ] || exit $rc; }
 step pytest 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 300 --timeout-method thread -x \
      -k "balanced_schedule or one_per_wave or kernel_info or config4_strong or 3-flat-20 or 3-flat-400 or device_batches"
-B="--no-cpu-baseline --handler-batch 0 --stream-steps 0"
+B="--no-cpu-baseline --handler-batch 0 --stream-steps 0 --no-general-leg"
 for s in auto one auto one; do
   step d20_$s 300 python -u bench.py --steps 20 --warmup 5 --schedule $s $B
   step s8_$s 300 python -u bench.py --steps 20 --warmup 5 --groups 125000 --schedule $s $B
