@@ -286,7 +286,9 @@ def parse_args(argv=None):
     ap.add_argument("--handler-batch", type=int, default=1_000_000,
                     help="messages per single-handler batch of the handler_batch leg (0 = skip the leg)")
     ap.add_argument("--handler-reps", type=int, default=20)
-    ap.add_argument("--handler-sample", type=int, default=128, help="groups checked against the oracle")
+    ap.add_argument("--handler-parity", type=int, default=20_000,
+                    help="messages of each kind in the handler leg's oracle-checked batch")
+    ap.add_argument("--handler-span", type=int, default=1024, help="groups the parity batch spans")
     ap.add_argument("--cpu-groups", type=int, default=20_000, help="calibration sample for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target seconds of the SoA leg on every core")
@@ -373,16 +375,72 @@ def handler_requests(rng, n, G, R, max_term):
     return group, dst, vote, app
 
 
+# the handler batches' algorithmic bytes per message: the
+# message in (group 8 + replica 4 + request), the response out, the replica's
+# 10 scalar fields read and written, and the two log slots its tail cache is
+# derived from; an append also reads log[prev] and writes its entry
+HANDLER_ALG_BYTES = {"vote": 12 + 16 + 8 + 2 * 40 + 16, "append": 12 + 32 + 12 + 2 * 40 + 16 + 8 + 8}
+HANDLER_PMC_FILE = os.path.join(ROOT, "profiles", "pmc_handler.json")
+
+
+def handler_parity(eng, O, params_kw, log_cap, kind, G, R, n_msgs, span, seed):
+    """The handler batch against the oracle's handlers on n_msgs messages over
+    `span` contiguous groups (several messages per replica, so runs of
+    messages to one replica are exercised): the span's state and logs copied
+    into one oracle, the batch applied by both, every response, state field
+    and log slot compared.  Returns (messages, mismatches)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    ga = int(rng.integers(0, max(1, G - span)))
+    st = eng.read_state(ga, span)
+    max_term = int(st[:, [r * abi.NUM_FIELDS + abi.F_INDEX["term"] for r in range(R)]].max())
+    group, dst, vote, app = handler_requests(rng, n_msgs, span, R, max_term)
+    group = group + ga
+    req = vote if kind == "vote" else app
+    t0, c0 = eng.read_log(ga, span)
+    o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(params_kw, G=span, g0=eng.g0 + ga)))
+    o.write_state(st)
+    o.write_log(t0, c0)
+    o.step_index = eng.step_index
+    dev = torch.device("cuda", eng.device)
+    w = 2 if kind == "vote" else 3
+    d_resp = torch.zeros((n_msgs, w), dtype=torch.int32, device=dev)
+    d_in = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (group, dst, req)]
+    fn = eng.vote_batch_dev if kind == "vote" else eng.append_batch_dev
+    fn(*(x.data_ptr() for x in d_in), d_resp.data_ptr(), n_msgs, after_stream=torch.cuda.current_stream(dev).cuda_stream)
+    resp = d_resp.cpu().numpy()
+    bad = 0
+    for m in range(n_msgs):
+        q, g = req[m], int(group[m]) - ga
+        if kind == "vote":
+            want = o.vote(g, int(dst[m]), *(int(x) for x in q))
+            bad += (int(resp[m, 0]), int(resp[m, 1])) != (int(want[0]), int(want[1]))
+        else:
+            qq = q.view(np.uint32).astype(np.int64)
+            t_, s_, st_ = o.append(g, int(dst[m]), int(q[0]), int(q[1]), int(q[2]), int(q[3]),
+                                   (int(q[5]), int(qq[6])) if q[4] else None, int(q[7]))
+            bad += tuple(int(x) for x in resp[m]) != (int(t_), int(s_), int(st_))
+    es, (et, ec) = eng.read_state(ga, span), eng.read_log(ga, span)
+    os_, (ot, oc) = o.read_state(), o.read_log()
+    bad += int(np.count_nonzero(np.any(es != os_, axis=1)))
+    phys = es[:, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(R)]]
+    slot = np.arange(log_cap)[None, None, :] < phys[:, :, None]
+    bad += int(np.count_nonzero(((et != ot) | (ec != oc)) & slot))
+    o.close()
+    return n_msgs, bad
+
+
 def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
     """The drop-in service path (RaftServer.vote() / append(), RaftServer.kt:228-287):
     raft_vote_batch_dev / raft_append_batch_dev on n random messages already
     in HBM (key, stable radix sort, one lane per replica run), and the same
     through the host entry points (from pageable arrays through pinned
-    staging, and from page-locked arrays by direct DMA).  The
-    first device batch of each kind is checked against the oracle's handlers
-    on a sample of groups: each sampled group's state and log are copied into
-    its own oracle, which applies the batch's messages to that group in batch
-    order; responses, state and logs must be equal."""
+    staging, and from page-locked arrays by direct DMA).  Parity: a batch of
+    --handler-parity messages of each kind on a span of groups against the
+    oracle's handlers (handler_parity).  Roofline: the algorithmic bytes per
+    message (HANDLER_ALG_BYTES) at the measured rate, and the rocprofv3 row of
+    the same batch (profiles/pmc_handler.json, scripts/pmc_handler.sh) when
+    one matches this kernel build."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -391,11 +449,15 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
     max_term = int(st[:, [r * abi.NUM_FIELDS + abi.F_INDEX["term"] for r in range(R)]].max())
     rng = np.random.default_rng(12345)
     group, dst, vote, app = handler_requests(rng, n, G, R, max_term)
-    sample = np.sort(rng.choice(G, size=min(G, args.handler_sample), replace=False))
-    t_step = eng.step_index
+    try:
+        pmc_rows = json.load(open(HANDLER_PMC_FILE))
+    except (OSError, ValueError):
+        pmc_rows = []
+    src = kernel_source_id()
     out = {"messages_per_batch": n, "groups": G, "replicas": R}
     for kind, req, resp_w in (("vote", vote, 2), ("append", app, 3)):
-        pre = {int(g): (eng.read_state(int(g), 1), *eng.read_log(int(g), 1)) for g in sample}
+        msgs, bad = handler_parity(eng, O, params_kw, log_cap, kind, G, R, args.handler_parity,
+                                   min(G, args.handler_span), 777 if kind == "vote" else 778)
         d_group = torch.from_numpy(group).to(dev)
         d_dst = torch.from_numpy(dst).to(dev)
         d_req = torch.from_numpy(np.ascontiguousarray(req)).to(dev)
@@ -403,37 +465,7 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         torch.cuda.synchronize(dev)
         fn = eng.vote_batch_dev if kind == "vote" else eng.append_batch_dev
         ptrs = (d_group.data_ptr(), d_dst.data_ptr(), d_req.data_ptr(), d_resp.data_ptr(), n)
-        fn(*ptrs)                                                       # the parity batch
-        resp = d_resp.cpu().numpy()
-        # oracle replay on the sample
-        sel = np.isin(group, sample)
-        bad = 0
-        for g in sample:
-            s0, t0, c0 = pre[int(g)]
-            o = O.Oracle(abi.make_params(log_cap=log_cap, **dict(params_kw, G=1, g0=int(g))))
-            o.write_state(s0)
-            o.write_log(t0, c0)
-            o.step_index = t_step
-            for m in np.nonzero(sel & (group == g))[0]:
-                q = req[m]
-                if kind == "vote":
-                    got = tuple(int(x) for x in resp[m])
-                    want = o.vote(0, int(dst[m]), *(int(x) for x in q))
-                    want = (int(want[0]), int(want[1]))
-                else:
-                    qq = q.view(np.uint32).astype(np.int64)
-                    t_, s_, st_ = o.append(0, int(dst[m]), int(q[0]), int(q[1]), int(q[2]), int(q[3]),
-                                           (int(q[5]), int(qq[6])) if q[4] else None, int(q[7]))
-                    got, want = tuple(int(x) for x in resp[m]), (int(t_), int(s_), int(st_))
-                bad += got != want
-            es, (et, ec) = eng.read_state(int(g), 1), eng.read_log(int(g), 1)
-            os_, (ot, oc) = o.read_state(), o.read_log()
-            bad += not np.array_equal(es, os_)
-            phys = es[0, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(R)]]
-            for r in range(R):
-                k = int(phys[r])
-                bad += not (np.array_equal(et[0, r, :k], ot[0, r, :k]) and np.array_equal(ec[0, r, :k], oc[0, r, :k]))
-            o.close()
+        fn(*ptrs)                                                       # warm (staging sized)
         # timed: device-resident batches (each call returns after its batch finished)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -442,11 +474,10 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         dt_dev = time.perf_counter() - t0
         # timed: host buffers (pinned staging + PCIe both ways)
         hfn = eng.vote_batch if kind == "vote" else eng.append_batch
-        hreq = req
         t0 = time.perf_counter()
         reps_h = max(1, args.handler_reps // 4)
         for _ in range(reps_h):
-            hfn(group, dst, hreq)
+            hfn(group, dst, req)
         dt_host = time.perf_counter() - t0
         # timed: page-locked host buffers (the engine's DMA reads and writes
         # the caller's arrays directly, no staging copy)
@@ -458,21 +489,37 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         for _ in range(args.handler_reps):
             hfn(pg, pd, pq, out=po)
         dt_pin = time.perf_counter() - t0
-        out[kind] = {"messages_per_s_device": n * args.handler_reps / dt_dev,
+        rate = n * args.handler_reps / dt_dev
+        ach = HANDLER_ALG_BYTES[kind] * rate / 1e9
+        pmc = next((r for r in pmc_rows if (r["kind"], r["n"], r["groups"], r["replicas"], r["kernel_src"])
+                    == (kind, n, G, R, src)), None)
+        out[kind] = {"messages_per_s_device": rate,
                      "ms_per_batch_device": dt_dev * 1e3 / args.handler_reps,
                      "messages_per_s_host_buffers": n * reps_h / dt_host,
                      "ms_per_batch_host_buffers": dt_host * 1e3 / reps_h,
                      "messages_per_s_pinned_host": n * args.handler_reps / dt_pin,
                      "ms_per_batch_pinned_host": dt_pin * 1e3 / args.handler_reps,
-                     "parity_sample_groups": int(sample.size), "parity_sample_messages": int(sel.sum()),
+                     "roofline": {"bound": "hbm", "alg_bytes_per_message": HANDLER_ALG_BYTES[kind],
+                                  "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": ach / HBM_PEAK_GBS,
+                                  "traffic_bytes_per_message": pmc["hbm_bytes_per_message"] if pmc else None,
+                                  "handler_kernel_traffic_bytes_per_message":
+                                      pmc["handler_kernel_hbm_bytes_per_message"] if pmc else None,
+                                  "traffic_frac": (pmc["hbm_bytes_per_message"] * rate / 1e9 / HBM_PEAK_GBS
+                                                   if pmc else None),
+                                  "pmc_source": pmc["source"] if pmc else None},
+                     "parity_messages": msgs, "parity_span_groups": min(G, args.handler_span),
                      "parity_mismatches": int(bad)}
     out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a key kernel, a stable hipcub radix sort "
                    "over the key bits, the handler kernel (one lane per replica run, messages in batch order) and "
                    "one status synchronisation; _host_buffers: the same through the host entry points from pageable "
                    "arrays (multi-threaded copy into engine-owned pinned staging, PCIe both ways); _pinned_host: from "
-                   "page-locked arrays, which the DMA reads and writes directly. The engine holds the bench run's final state; the messages are "
-                   "random (bench.handler_requests). Parity: the first batch of each kind against the oracle's "
-                   "handlers on the sampled groups")
+                   "page-locked arrays, which the DMA reads and writes directly. The engine holds the bench run's "
+                   "final state; the messages are random (bench.handler_requests). roofline: the algorithmic bytes "
+                   "per message (message in, response out, the replica's fields read and written, its tail-cache "
+                   "slots; an append's log[prev] read and entry write) at the device rate; traffic: rocprofv3 "
+                   "FETCH_SIZE + WRITE_SIZE of every kernel of the batch per message. Parity: a separate batch of "
+                   "parity_messages messages over a span of groups, replayed by the oracle's handlers")
     return out
 
 
@@ -832,6 +879,9 @@ def main(argv=None, result=None):
         # step-kernel dispatch per sub-range; the streaming leg runs one range
         seq = [["warmup", x, nsub] for x in launch_plan(args.warmup, L)] + [["timed", x, nsub] for x in timed_plan]
         seq += [["streaming", 1, 1]] * args.stream_steps
+        if general is not None:                   # the general kernel replays the warmup and timed launches
+            seq += [["general_warmup", x, nsub] for x in launch_plan(args.warmup, L)]
+            seq += [["general", x, nsub] for x in timed_plan]
         json.dump({"key": pmc_key, "stream_steps": args.stream_steps, "R": R, "launches": seq},
                   open(args.plan_file, "w"))
 

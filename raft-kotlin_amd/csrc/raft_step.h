@@ -286,6 +286,23 @@ struct PhaseClock {
 #endif
 };
 
+// Phase budget (diagnostic builds only, -DRAFT_PHASE_TWICE=1 + PH_x): phase
+// x runs a second time first, on copies of the node, context and counters
+// whose results are sunk, so SQ_INSTS_VALU / SALU of that build minus the
+// product build's is the phase's dynamic instruction count (DESIGN.md §4.5,
+// scripts/phase_budget.sh).  Never compiled into the product build.
+#ifndef RAFT_PHASE_TWICE
+#define RAFT_PHASE_TWICE 0
+#endif
+#define RAFT_TWICE(PH, CALL)                                                        \
+    if constexpr (RAFT_PHASE_TWICE == (PH) + 1) {                                  \
+        auto c2 = c;                                                               \
+        auto n2 = n;                                                               \
+        auto k2 = cnt;                                                             \
+        CALL;                                                                      \
+        sink_copy(n2, k2);                                                         \
+    }
+
 // One replica's scalar state, by reference.
 struct Rep {
     int32_t &term, &voted, &role, &commit, &last, &phys, &elec, &phase, &retry;
@@ -518,6 +535,16 @@ struct Node {
         return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl, t1, t2, c1};
     }
 };
+
+// keeps a phase copy's results alive (RAFT_PHASE_TWICE builds)
+template <class NODE, class CNT>
+__device__ __forceinline__ void sink_copy(const NODE& n, const CNT& k) {
+    asm volatile("" ::"v"(n.term), "v"(n.voted), "v"(n.role), "v"(n.commit), "v"(n.last), "v"(n.phys));
+    asm volatile("" ::"v"(n.elec), "v"(n.phase), "v"(n.retry), "v"(n.fl), "v"(n.t1), "v"(n.t2), "v"(n.c1));
+    asm volatile("" ::"v"(n.nx), "v"(n.mc), "v"(n.iso), "v"(n.cmdc), "v"(n.s0));
+#pragma unroll
+    for (int i = 0; i < NCW; ++i) asm volatile("" ::"s"(k.s[i]));
+}
 
 template <int R>
 struct Lanes {
@@ -1124,60 +1151,67 @@ struct Stepper {
         // role changes between K and the next T), made at launch start
         const uint32_t lead0 = c.lead;
 
-        // ---------------- T: timers and election clocks ----------------
         uint32_t send;
         int32_t qt, qli, qlt;
         uint64_t sstart;
-        // a wave where no timer fires and no replica is electing only counts
-        // its armed timers down (most waves in steady state)
-        const int32_t P = p.P;
-        const uint64_t t_armed = lm(n.fl & FL_ARMED);
-        const int32_t t_el = n.elec - P;
-        const uint64_t t_fire = t_armed & lm(t_el <= 0);                    // Commons.kt:25-27
-        const uint64_t electing = lm(n.fl & FL_ELECTING);                   // T does not change it before use
-        if (!(t_fire | electing)) {
-            n.elec = ib(t_armed) ? t_el : n.elec;
-            send = 0u; sstart = 0; qt = qli = qlt = 0;
-        } else {
-            uint32_t f = n.fl;
-            const bool fire = ib(t_fire);
-            n.elec = ib(t_armed) ? (fire ? 0 : t_el) : n.elec;
-            f &= fire ? ~FL_ARMED : ~0u;
-            n.role = fire ? (int32_t)RAFT_CANDIDATE : n.role;               // RaftServer.kt:182
-            cnt.add(t_fire, RAFT_C_TIMEOUTS);
-            const uint64_t backoff = lm(f & FL_BACKOFF);
-            const uint64_t start_fire = t_fire & ~electing;                 // offer(CANDIDATE) :184 -> :65
-            const uint64_t in_round = electing & ~backoff, in_bo = electing & backoff;
-            const int32_t ph = n.phase + (ib(in_round) ? P : (ib(in_bo) ? -P : 0));   // latch clock :214 / delay :221
-            const uint32_t pend = (f >> PEND_SH) & 0xFFu;
-            const uint64_t rtick = in_round & lm(pend != 0) & lm(ph < p.round_to);
-            const int32_t rty = n.retry - (ib(rtick) ? P : 0);             // retry delay, Commons.kt:43
-            const uint64_t resend = rtick & lm(rty <= 0);
-            const uint64_t bo_end = in_bo & lm(ph <= 0);
-            const uint64_t restart = bo_end & lm(n.role == RAFT_CANDIDATE); // while (state == CANDIDATE) :191
-            const uint64_t endel = bo_end & ~restart;
-            const uint64_t sr = start_fire | restart;                       // round head :191-199
-            const bool bsr = ib(sr), bend = ib(endel);
-            n.term = inc_if(n.term, sr);                                    // :192
-            n.voted = bsr ? r + 1 : n.voted;                                // :193
-            const uint32_t fr = (f & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
-                                (ALL << PEND_SH) | (ib(start_fire) ? FL_ELECTING : 0u);
-            uint32_t fe = f;                                                // the flags of an election that ends
-            if (RARE(endel)) fe = end_flags(f, n.role);                     // (rare: ~9 VALU skipped)
-            n.fl = bsr ? fr : (bend ? fe : f);
-            n.phase = (bsr || bend) ? 0 : ph;
-            n.retry = (bsr || bend) ? 0 : rty;
-            sstart = endel & lm(n.role == RAFT_LEADER);
-            send = bsr ? ALL : (ib(resend) ? pend : 0u);
-            // the RequestVote snapshot, built inside retry{} (:200-207)
-            qt = n.term;
-            qli = n.last;
-            qlt = n.last != 0 ? n.t1 : 0;
-            cnt.add((sr | resend) & lm(n.last != 0), RAFT_C_VOTE_LOG_READS);
-            if constexpr (RING) cnt.add((sr | resend) & lm(n.last != 0) & lm(n.phys - n.last >= p.W), RAFT_C_LOG_WINDOW_MISS);
-            cnt.add(sr, RAFT_C_ROUNDS);
-        }
-        start_sessions(p, c, n, sstart, cnt);
+        auto phase_t = [&](Ctx<R>& c, Node& n, Counters& cnt, uint32_t& send, int32_t& qt, int32_t& qli, int32_t& qlt,
+                           uint64_t& sstart) {
+            // ---------------- T: timers and election clocks ----------------
+            // a wave where no timer fires and no replica is electing only counts
+            // its armed timers down (most waves in steady state)
+            const int32_t P = p.P;
+            const uint64_t t_armed = lm(n.fl & FL_ARMED);
+            const int32_t t_el = n.elec - P;
+            const uint64_t t_fire = t_armed & lm(t_el <= 0);                    // Commons.kt:25-27
+            const uint64_t electing = lm(n.fl & FL_ELECTING);                   // T does not change it before use
+            if (!(t_fire | electing)) {
+                n.elec = ib(t_armed) ? t_el : n.elec;
+                send = 0u; sstart = 0; qt = qli = qlt = 0;
+            } else {
+                uint32_t f = n.fl;
+                const bool fire = ib(t_fire);
+                n.elec = ib(t_armed) ? (fire ? 0 : t_el) : n.elec;
+                f &= fire ? ~FL_ARMED : ~0u;
+                n.role = fire ? (int32_t)RAFT_CANDIDATE : n.role;               // RaftServer.kt:182
+                cnt.add(t_fire, RAFT_C_TIMEOUTS);
+                const uint64_t backoff = lm(f & FL_BACKOFF);
+                const uint64_t start_fire = t_fire & ~electing;                 // offer(CANDIDATE) :184 -> :65
+                const uint64_t in_round = electing & ~backoff, in_bo = electing & backoff;
+                const int32_t ph = n.phase + (ib(in_round) ? P : (ib(in_bo) ? -P : 0));   // latch clock :214 / delay :221
+                const uint32_t pend = (f >> PEND_SH) & 0xFFu;
+                const uint64_t rtick = in_round & lm(pend != 0) & lm(ph < p.round_to);
+                const int32_t rty = n.retry - (ib(rtick) ? P : 0);             // retry delay, Commons.kt:43
+                const uint64_t resend = rtick & lm(rty <= 0);
+                const uint64_t bo_end = in_bo & lm(ph <= 0);
+                const uint64_t restart = bo_end & lm(n.role == RAFT_CANDIDATE); // while (state == CANDIDATE) :191
+                const uint64_t endel = bo_end & ~restart;
+                const uint64_t sr = start_fire | restart;                       // round head :191-199
+                const bool bsr = ib(sr), bend = ib(endel);
+                n.term = inc_if(n.term, sr);                                    // :192
+                n.voted = bsr ? r + 1 : n.voted;                                // :193
+                const uint32_t fr = (f & ~(FL_BACKOFF | (0xFFu << PEND_SH) | (0xFu << VOTES_SH) | (0xFu << LATCH_SH))) |
+                                    (ALL << PEND_SH) | (ib(start_fire) ? FL_ELECTING : 0u);
+                uint32_t fe = f;                                                // the flags of an election that ends
+                if (RARE(endel)) fe = end_flags(f, n.role);                     // (rare: ~9 VALU skipped)
+                n.fl = bsr ? fr : (bend ? fe : f);
+                n.phase = (bsr || bend) ? 0 : ph;
+                n.retry = (bsr || bend) ? 0 : rty;
+                sstart = endel & lm(n.role == RAFT_LEADER);
+                send = bsr ? ALL : (ib(resend) ? pend : 0u);
+                // the RequestVote snapshot, built inside retry{} (:200-207)
+                qt = n.term;
+                qli = n.last;
+                qlt = n.last != 0 ? n.t1 : 0;
+                cnt.add((sr | resend) & lm(n.last != 0), RAFT_C_VOTE_LOG_READS);
+                if constexpr (RING) cnt.add((sr | resend) & lm(n.last != 0) & lm(n.phys - n.last >= p.W), RAFT_C_LOG_WINDOW_MISS);
+                cnt.add(sr, RAFT_C_ROUNDS);
+            }
+            start_sessions(p, c, n, sstart, cnt);
+        };
+        RAFT_TWICE(PH_T, ({ uint32_t s_; int32_t a_, b_, d_; uint64_t e_;
+                            phase_t(c2, n2, k2, s_, a_, b_, d_, e_);
+                            asm volatile("" ::"v"(s_), "v"(a_), "v"(b_), "v"(d_), "s"(e_)); }));
+        phase_t(c, n, cnt, send, qt, qli, qlt, sstart);
         c.clk.mark(PH_T);
 
         // ---------------- the step's Philox pass (S-9) ----------------
@@ -1215,6 +1249,9 @@ struct Stepper {
             // every lane's constant purpose and keeps those products in VGPRs
             // across the step loop (R = 7 spilled them to scratch)
             asm volatile("" : "+v"(purpose));
+            RAFT_TWICE(PH_JOBS, ({ uint32_t z = 0; asm volatile("" : "+v"(z));
+                                   const u32x4 w = kdraw(p, c.t, c.gid(), purpose ^ z, sub);
+                                   asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w)); }));
             c.job = kdraw(p, c.t, c.gid(), purpose, sub);
             // stage the wave's jobs in LDS (one ds_write_b128 per lane); a
             // wave's LDS accesses complete in order, so its reads below see
@@ -1266,34 +1303,37 @@ struct Stepper {
         // senders -- usually one -- with one handler per destination lane.
         // the lanes of groups with a pending sender: each round's predicate
         // and the loop condition (one ballot per round)
-        uint64_t mv = lm(vtodo != 0);
-        if (mv) {
-            // RING: the replicas whose log.get(lastIndex - 1) is below the
-            // window; hasl: lastIndex >= 1 (the vote handlers do not touch the
-            // logs, so both hold for the whole phase)
-            const uint64_t gapw = RING ? lm(n.phys - n.last >= p.W) : 0ull;
-            const uint64_t hasl = lm(n.last >= 1);
-            const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during V
-            if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
-                // the job lanes do not hold the first sender's chunk (R < 4):
-                // one staging pass serves every round, the first included
-                stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
-                do {
-                    vote_round<true>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
-                    mv = lm(vtodo != 0);
-                } while (mv);
-            } else {
-                vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
-                mv = lm(vtodo != 0);
-                if (mv) {                                                   // groups with 2+ senders
-                    if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
+        auto phase_v = [&](Ctx<R>& c, Node& n, Counters& cnt, uint32_t vtodo, uint64_t mv) {
+            if (mv) {
+                // RING: the replicas whose log.get(lastIndex - 1) is below the
+                // window; hasl: lastIndex >= 1 (the vote handlers do not touch the
+                // logs, so both hold for the whole phase)
+                const uint64_t gapw = RING ? lm(n.phys - n.last >= p.W) : 0ull;
+                const uint64_t hasl = lm(n.last >= 1);
+                const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during V
+                if constexpr (L::SENDERS_STAGED && !L::VOTE_JOB) {
+                    // the job lanes do not hold the first sender's chunk (R < 4):
+                    // one staging pass serves every round, the first included
+                    stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
                     do {
-                        vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
+                        vote_round<true>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
                         mv = lm(vtodo != 0);
                     } while (mv);
+                } else {
+                    vote_round(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
+                    mv = lm(vtodo != 0);
+                    if (mv) {                                                   // groups with 2+ senders
+                        if constexpr (L::SENDERS_STAGED) stage_sender_chunks(p, c, RAFT_RNG_VOTE_DROP);
+                        do {
+                            vote_round<L::SENDERS_STAGED>(p, c, n, cnt, vtodo, mv, send, qt, qli, qlt, gapw, hasl, fs);
+                            mv = lm(vtodo != 0);
+                        } while (mv);
+                    }
                 }
             }
-        }
+        };
+        RAFT_TWICE(PH_V, phase_v(c2, n2, k2, vtodo, lm(vtodo != 0)));
+        phase_v(c, n, cnt, vtodo, lm(vtodo != 0));
 
         c.clk.mark(PH_V);
         // ---------------- D: latch closes -> decision (RaftServer.kt:214-222) ----------------
@@ -1339,30 +1379,33 @@ struct Stepper {
         // the compiler carry the counters in VGPRs and copy the node per round).
         // mt: the lanes of groups with a session left to tick (each round's
         // predicate and the loop condition, one ballot per round)
-        uint64_t mt = lm(todo != 0);
-        if (LIKELY(mt)) {
-            const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during A
-            {
-                // R = 2: the job lanes do not hold the first leader's chunk,
-                // so one staging pass serves every round, the first included
-                constexpr bool FIRST_STAGED = L::SENDERS_STAGED && !L::TICK_JOB;
-                if constexpr (FIRST_STAGED) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
-                const int s = ib(mt) ? __builtin_ctz(todo) : 0;
-                todo &= todo - 1u;
-                tick<FIRST_STAGED>(p, c, n, mt, s, fs, cnt);
-            }
-            mt = lm(todo != 0);
-            if (RARE(mt)) {                                                 // 2+ sessions (rare)
-                constexpr bool ALL = L::SENDERS_STAGED;
-                if constexpr (ALL && L::TICK_JOB) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
-                do {
+        auto phase_a = [&](Ctx<R>& c, Node& n, Counters& cnt, uint32_t todo, uint64_t mt) {
+            if (LIKELY(mt)) {
+                const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during A
+                {
+                    // R = 2: the job lanes do not hold the first leader's chunk,
+                    // so one staging pass serves every round, the first included
+                    constexpr bool FIRST_STAGED = L::SENDERS_STAGED && !L::TICK_JOB;
+                    if constexpr (FIRST_STAGED) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
                     const int s = ib(mt) ? __builtin_ctz(todo) : 0;
                     todo &= todo - 1u;
-                    tick<ALL>(p, c, n, mt, s, fs, cnt);
-                    mt = lm(todo != 0);
-                } while (mt);
+                    tick<FIRST_STAGED>(p, c, n, mt, s, fs, cnt);
+                }
+                mt = lm(todo != 0);
+                if (RARE(mt)) {                                                 // 2+ sessions (rare)
+                    constexpr bool ALL = L::SENDERS_STAGED;
+                    if constexpr (ALL && L::TICK_JOB) stage_sender_chunks(p, c, RAFT_RNG_APPEND_DROP);
+                    do {
+                        const int s = ib(mt) ? __builtin_ctz(todo) : 0;
+                        todo &= todo - 1u;
+                        tick<ALL>(p, c, n, mt, s, fs, cnt);
+                        mt = lm(todo != 0);
+                    } while (mt);
+                }
             }
-        }
+        };
+        RAFT_TWICE(PH_A, phase_a(c2, n2, k2, todo, lm(todo != 0)));
+        phase_a(c, n, cnt, todo, lm(todo != 0));
 
         c.clk.mark(PH_A);
         // ---------------- C: client commands (S-11) ----------------
@@ -1371,15 +1414,19 @@ struct Stepper {
         const uint32_t lead = c.gbits(isl);
         const KernArgs kp = kernargs();
         const uint64_t cmd_thr = kp->cmd_thr32;
-        if (cmd_thr) {
-            const int32_t cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
-            constexpr bool CL = (NET & NET_CMDLOW) != 0;                   // lowest LEADER, no limit
-            const uint64_t cm = (CL || cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) &
-                                lm((uint64_t)hw1 < cmd_thr) & lm(lead != 0);
-            const uint64_t tgt = cm & (CL || cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
-            append_command<TB, RING>(n.rep(), tgt, c.template log<RING>(p), hw2, cnt);
-            n.cmdc = inc_if(n.cmdc, cm);
-        }
+        auto phase_c = [&](Ctx<R>& c, Node& n, Counters& cnt) {
+            if (cmd_thr) {
+                const int32_t cmd_limit = kp->cmd_limit, cmd_mode = kp->cmd_mode;
+                constexpr bool CL = (NET & NET_CMDLOW) != 0;                   // lowest LEADER, no limit
+                const uint64_t cm = (CL || cmd_limit == 0 ? ~0ull : lm(n.cmdc < cmd_limit)) &
+                                    lm((uint64_t)hw1 < cmd_thr) & lm(lead != 0);
+                const uint64_t tgt = cm & (CL || cmd_mode == RAFT_CMD_LOWEST_LEADER ? lm(r == __builtin_ctz(lead)) : isl);
+                append_command<TB, RING>(n.rep(), tgt, c.template log<RING>(p), hw2, cnt);
+                n.cmdc = inc_if(n.cmdc, cm);
+            }
+        };
+        RAFT_TWICE(PH_C, phase_c(c2, n2, k2));
+        phase_c(c, n, cnt);
 
         c.clk.mark(PH_C);
         // ---------------- K: end-of-step observations ----------------

@@ -1,0 +1,109 @@
+"""Parse scripts/pmc_handler.sh output: per handler batch (a batch_keys_kernel
+dispatch starts one) the HBM bytes of all its kernels (keys, the hipcub radix
+sort, batch_kernel) and of batch_kernel alone, from FETCH_SIZE / WRITE_SIZE
+with the calibration engine's counter-to-bytes factors (scripts/pmc_parse.py),
+and the kernels' durations from the trace.  Rows (one per batch kind) ->
+<dir>/handler_rows.json; `--merge` folds them into profiles/pmc_handler.json,
+which bench.py's handler_batch leg reads."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import pmc_parse  # noqa: E402
+
+OUT_FILE = os.path.join(ROOT, "profiles", "pmc_handler.json")
+
+
+def kernels(d, counter=None):
+    """[(dispatch id, kernel name, value)] in dispatch order: the counter's
+    value (rows of one dispatch summed) or, without a counter, the duration (ns)."""
+    acc = defaultdict(float)
+    name = {}
+    if counter:
+        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            for row in csv.DictReader(open(f)):
+                if row["Counter_Name"] == counter:
+                    k = int(row["Dispatch_Id"])
+                    acc[k] += float(row["Counter_Value"])
+                    name[k] = row["Kernel_Name"]
+    else:
+        for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+            for row in csv.DictReader(open(f)):
+                k = int(row["Dispatch_Id"])
+                acc[k] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                name[k] = row["Kernel_Name"]
+    return [(k, name[k], acc[k]) for k in sorted(acc)]
+
+
+def batches(rows):
+    """Group a dispatch list into handler batches: each starts at a batch_keys_kernel."""
+    out, cur = [], None
+    for _, n, v in rows:
+        if "batch_keys_kernel" in n:
+            cur = []
+            out.append(cur)
+        if cur is not None:
+            cur.append((n, v))
+    return out
+
+
+def main(d):
+    plan = json.loads([ln for ln in open(f"{d}/trace.log") if ln.startswith("{")][-1])
+    state = pmc_parse.CALIB_G * (pmc_parse.CALIB_R * pmc_parse.REPLICA_BYTES + pmc_parse.GROUP_BYTES)
+    cf = sorted(pmc_parse.dispatches(f"{d}/calib_FETCH_SIZE").get("FETCH_SIZE", []))
+    cw = sorted(pmc_parse.dispatches(f"{d}/calib_WRITE_SIZE").get("WRITE_SIZE", []))
+    ff, wf = state / (cf[len(cf) // 2] * 1024.0), state / (cw[len(cw) // 2] * 1024.0)
+    fb, wb, tb = (batches(kernels(f"{d}/pmc_FETCH_SIZE", "FETCH_SIZE")),
+                  batches(kernels(f"{d}/pmc_WRITE_SIZE", "WRITE_SIZE")), batches(kernels(f"{d}/trace")))
+    kinds = [k for k, reps in plan["plan"] for _ in range(reps)]
+    if not (len(fb) == len(wb) == len(tb) == len(kinds)):
+        raise SystemExit(f"batches: fetch {len(fb)} write {len(wb)} trace {len(tb)} plan {len(kinds)}")
+    rows = []
+    for kind in dict.fromkeys(kinds):
+        ix = [i for i, k in enumerate(kinds) if k == kind][1:] or [kinds.index(kind)]   # the first is a warmup
+        n = plan["n"]
+
+        def avg(bl, sel=lambda nm: True):
+            return sum(sum(v for nm, v in bl[i] if sel(nm)) for i in ix) / len(ix)
+        hk = lambda nm: "batch_kernel" in nm  # noqa: E731
+        fetch, write = avg(fb) * 1024 * ff, avg(wb) * 1024 * wf
+        hfetch, hwrite = avg(fb, hk) * 1024 * ff, avg(wb, hk) * 1024 * wf
+        t_all, t_h = avg(tb) / 1e6, avg(tb, hk) / 1e6
+        rows.append({"kind": kind, "n": n, "groups": plan["groups"], "replicas": plan["replicas"],
+                     "kernel_src": plan["kernel_src"], "batches_averaged": len(ix),
+                     "hbm_bytes_per_batch": fetch + write, "hbm_bytes_per_message": (fetch + write) / n,
+                     "handler_kernel_hbm_bytes_per_message": (hfetch + hwrite) / n,
+                     "handler_kernel_fetch_bytes": hfetch, "handler_kernel_write_bytes": hwrite,
+                     "kernels_ms_per_batch": t_all, "handler_kernel_ms": t_h,
+                     "handler_kernel_hbm_gbs": (hfetch + hwrite) / (t_h / 1e3) / 1e9 if t_h else None,
+                     "kernels_per_batch": [nm.split("(")[0][-60:] for nm, _ in tb[ix[0]]],
+                     "fetch_factor": ff, "write_factor": wf,
+                     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes + --kernel-trace "
+                               f"(scripts/pmc_handler.sh, {os.path.basename(d)})"})
+    json.dump(rows, open(os.path.join(d, "handler_rows.json"), "w"), indent=1)
+    print(json.dumps(rows, indent=1))
+
+
+def merge(files):
+    try:
+        have = json.load(open(OUT_FILE))
+    except (OSError, ValueError):
+        have = []
+    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"], r["kernel_src"])  # noqa: E731
+    out = {key(r): r for r in have}
+    for f in files:
+        for r in json.load(open(f)):
+            out[key(r)] = r
+    json.dump(list(out.values()), open(OUT_FILE, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--merge":
+        merge(sys.argv[2:])
+    else:
+        main(sys.argv[1])

@@ -93,7 +93,7 @@ def main(d):
             per[c] = acc
     trd = traced(d)
     rows = []
-    for leg in ("timed", "streaming"):
+    for leg in ("timed", "streaming", "general"):
         ix = [i for i, x in enumerate(seq) if x[0] == leg]
         if not ix:
             continue
