@@ -823,8 +823,10 @@ def main(argv=None, result=None):
         roofline_valu = {
             "bound": "valu", "achieved": ips, "peak": VALU_PEAK_GIPS, "unit": "G wave-instructions/s",
             "frac": ips / VALU_PEAK_GIPS,
-            "valu_per_wave_step": pmc["valu_per_launch"] / (pmc["waves"] * L),
-            "salu_per_wave_step": pmc["salu_per_launch"] / (pmc["waves"] * L),
+            # per chunk-step: one wave's 64 // R groups for one step (a launch of
+            # the balanced schedule runs fewer, longer-lived waves than chunks)
+            "valu_per_wave_step": pmc["valu_per_launch"] / (-(-G_local // (64 // R)) * L),
+            "salu_per_wave_step": pmc["salu_per_launch"] / (-(-G_local // (64 // R)) * L),
             "valu_per_simd_cycle": pmc["valu_per_launch"] / (SIMDS * CLOCK_HZ * kern_avg_ms / 1e3),
             "simd_cycles_per_valu": SIMDS * clk * 1e9 * kern_avg_ms / 1e3 / pmc["valu_per_launch"],
             "effective_clock_ghz": clk,

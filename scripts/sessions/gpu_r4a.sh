@@ -18,4 +18,5 @@ step def_auto 400 python -u bench.py $B
 step def_one3 400 python -u bench.py --schedule one --subranges 3 $B
 step s8def_auto 400 python -u bench.py --groups 125000 $B
 step s8def_one3 400 python -u bench.py --groups 125000 --schedule one --subranges 3 $B
+TAG=r4a bash scripts/phase_budget.sh; echo "phase rc=$?" >> $OUT/status.txt
 exit 0
