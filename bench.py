@@ -269,6 +269,8 @@ def parse_args(argv=None):
                          "0 = the kernel variant's default (abi.bench_steps_per_launch)")
     ap.add_argument("--subranges", type=int, default=0,
                     help="step-kernel launch sub-ranges, each on its own stream (0 = the engine's automatic choice)")
+    ap.add_argument("--schedule-workgroups", type=int, default=0,
+                    help="workgroups of a balanced launch (0 = the resident workgroups; tuning)")
     ap.add_argument("--schedule", choices=["auto", "one", "balanced"], default="auto",
                     help="step-kernel schedule (raft_params.schedule): balanced when the chunks outnumber the "
                          "resident wave slots (auto), one chunk per wave, or balanced")
@@ -627,7 +629,7 @@ def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, s
     flat = -(-G // (64 // R)) * 64 * log_cap * 8
     window = 0 if flat <= 0.6 * torch.cuda.get_device_properties(dev).total_memory else 256
     params = abi.make_params(log_cap=max(log_cap, window), log_window=window, steps_per_launch=L, mode=mode,
-                             subranges=args.subranges, schedule=SCHEDULES[args.schedule],
+                             subranges=args.subranges, schedule=SCHEDULES[args.schedule], schedule_workgroups=args.schedule_workgroups,
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges
@@ -780,7 +782,7 @@ def main(argv=None, result=None):
     # schedule ends a launch's waves together)
     subranges = args.subranges
     params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=subranges,
-                             schedule=SCHEDULES[args.schedule],
+                             schedule=SCHEDULES[args.schedule], schedule_workgroups=args.schedule_workgroups,
                              ae_max_entries=args.ae_max_entries, **dict(kw, G=G_local, g0=g0))
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs

@@ -41,6 +41,12 @@ constexpr int BLOCK = 256;
 #ifdef RAFT_PROFILE_PHASES
 __device__ unsigned long long g_phase_cycles[PH_N];   // diagnostic builds only
 #endif
+#ifdef RAFT_WAVE_TIMES
+// diagnostic builds only: per wave of the last step launch, its start and end
+// (s_memrealtime, 100 MHz, chip-wide) and its HW_ID / XCC_ID registers
+constexpr int WT_MAX = 1 << 17;
+__device__ unsigned long long g_wave_times[WT_MAX][3];
+#endif
 constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 // step_kernel's workgroup: its LDS holds one counter row per step for the
 // whole workgroup, so larger workgroups leave room for longer launches
@@ -52,7 +58,7 @@ constexpr int STEP_WAVES = STEP_BLOCK / 64;
 constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
 constexpr int TALLY_LDS_WORDS = STEP_WAVES * 16;          // per-wave vote-tally words (Ctx::tl, R >= 4)
 constexpr int FLAG_LDS_WORDS = STEP_WAVES;                // balanced schedule: a wave's head piece is stored
-constexpr int PLAN_LDS_WORDS = STEP_WAVES * 4;            // each wave's plan (plan_of)
+constexpr int PLAN_LDS_WORDS = STEP_WAVES * 8;            // each wave's plan (plan_of) and priority bands
 constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS + FLAG_LDS_WORDS + PLAN_LDS_WORDS;
 // the longest launch whose LDS (job rows, tally words, K counter rows) still
 // lets 7 step workgroups share a CU's 160 KB
@@ -225,18 +231,25 @@ __device__ __forceinline__ uint4 plan_of(int wib, int K) {
     const KernArgs kp = kernargs();
     if (kp->bal_chunks == 0)
         return make_uint4(0u, (uint32_t)(kp->wave0 + (int32_t)blockIdx.x * STEP_WAVES + wib), 1u, 0u);
-    // workgroup b: chunks [c0, c0 + m), m = q or q + 1 (q = n / nb, the first
-    // n % nb workgroups take one more); 32-bit throughout (the host keeps
-    // m * K < 2^31)
+    // workgroup b: its i-th chunk is wave0 + b + i * nb (piece_chunk), i < m,
+    // m = q or q + 1 (q = n / nb, the first n % nb workgroups take one more):
+    // the chunks running at one time are neighbours, as in the one-chunk-per-
+    // wave schedule; the plan holds indices i; 32-bit throughout (the host
+    // keeps m * K < 2^31)
     const uint32_t b = blockIdx.x, q = (uint32_t)kp->bal_q, rem = (uint32_t)kp->bal_rem, k = (uint32_t)K;
-    const uint32_t c0 = (uint32_t)kp->wave0 + b * q + min(b, rem);
     const uint32_t U = (q + (b < rem ? 1u : 0u)) * k;
     const uint32_t u0 = (uint32_t)wib * U / STEP_WAVES, u1 = (uint32_t)(wib + 1) * U / STEP_WAVES;
     const uint32_t a = u0 / k, s = u0 - a * k, z = u1 / k, e = u1 - z * k;
     const uint32_t f = a + (s != 0);
-    return make_uint4(e, c0 + f, z - f, s);
+    return make_uint4(e, f, z - f, s);
 }
 __device__ __forceinline__ int n_pieces(uint4 pl) { return (pl.x != 0) + (int)pl.z + (pl.w != 0); }
+// the chunk of a piece: the one-chunk-per-wave plan holds it, a balanced
+// plan the workgroup's chunk index i (plan_of)
+__device__ __forceinline__ int piece_chunk(int32_t i) {
+    const KernArgs kp = kernargs();
+    return kp->bal_chunks == 0 ? i : kp->wave0 + (int32_t)blockIdx.x + i * (int32_t)gridDim.x;
+}
 __device__ __forceinline__ Piece piece_of(uint4 pl, int q, int K) {
     const int32_t e = (int32_t)pl.x, f = (int32_t)pl.y, nf = (int32_t)pl.z, s = (int32_t)pl.w;
     if (e != 0) {
@@ -246,6 +259,34 @@ __device__ __forceinline__ Piece piece_of(uint4 pl, int q, int K) {
     if (q < nf) return Piece{f + q, 0, K, false, false};                           // whole chunks
     return Piece{f - 1, s, K, true, false};                                        // tail
 }
+// Issue priority of a wave of the balanced schedule (s_setprio, 3 = the
+// highest).  A SIMD's arbiter issues from the oldest ready wave of the
+// highest priority, so among long-lived waves of equal work the oldest race
+// ahead and the youngest starve until they are left alone at low occupancy
+// (measured: waves of equal work ended between 560 and 1,278 us of a 1.28 ms
+// launch, profiles/r4_a3).  Each wave therefore starts at 3 and steps down as
+// its own work runs out (bands of 1/2, 1/4, 3/20 of it, then the last 1/10),
+// so a wave that got ahead yields to the ones behind it.
+__device__ __forceinline__ void set_priority(int band) {
+    if (band >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (band == 2) __builtin_amdgcn_s_setprio(2);
+    else if (band == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+// a wave's chunk-steps from its plan (balanced schedule)
+__device__ __forceinline__ uint32_t plan_units(uint4 pl, int K) {
+    return pl.x + pl.z * (uint32_t)K + (pl.w != 0 ? (uint32_t)K - pl.w : 0u);
+}
+// chunk-steps from the start of the wave's quarter to the end of band b (b =
+// 3, 2, 1), per mille of its work (tuning builds set other ends)
+#ifndef RAFT_BAND_ENDS
+#define RAFT_BAND_ENDS 500, 750, 900
+#endif
+__device__ __forceinline__ uint32_t band_end(uint32_t Q, int b) {
+    constexpr uint32_t E[3] = {RAFT_BAND_ENDS};
+    return (uint32_t)(((uint64_t)Q * E[3 - b]) / 1000u);
+}
+
 // Bounded wait for the previous wave's head piece (never reached by a correct
 // schedule without the flag set; the bound keeps a broken one from hanging the
 // GPU -- its results would then differ from the oracle's).  The flag is set
@@ -300,6 +341,9 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     const int j = lane / R;
     const int r = lane - j * R;
 
+#ifdef RAFT_WAVE_TIMES
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
     if (threadIdx.x < FLAG_LDS_WORDS) lds_flag[threadIdx.x] = 0u;
     __syncthreads();                                                      // counter rows and flags zeroed
@@ -324,11 +368,18 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     // +600 static VALU at R = 5.)
     int pc = 0;                                    // this wave's current piece
     int k, k1, k0;                                 // its step, the step it ends before, its first step
+    int band_left;                                 // chunk-steps to the next priority band (balanced)
     {   // (a wave's first piece is never a tail: a wave runs its head first)
         const uint4 pl = plan_of(wib, nsteps);
-        *(uint4*)(lds_plan + wib * 4) = pl;
+        *(uint4*)(lds_plan + wib * 8) = pl;
+        const bool bal = kernargs()->bal_chunks != 0;
+        const uint32_t Q = plan_units(pl, nsteps);
+        // [4]: the band now, [5]: chunk-steps done at its start, [6]: Q
+        *(uint4*)(lds_plan + wib * 8 + 4) = make_uint4(3u, 0u, Q, 0u);
+        band_left = bal ? (int)band_end(Q, 3) : 0x7FFFFFFF;
+        if (bal) set_priority(3);
         const Piece pz = piece_of(pl, 0, nsteps);
-        enter_piece<R, RING>(c, n, pz.chunk);
+        enter_piece<R, RING>(c, n, piece_chunk(pz.chunk));
         k = k0 = pz.k0;
         k1 = pz.k1;
     }
@@ -374,6 +425,15 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         if (ib((1ull << NCW) - 1))
             __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         c.clk.mark(PH_CNT);
+        if (RARE(--band_left == 0)) {              // this wave's next priority band (balanced)
+            const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
+            uint4 bs = *(const uint4*)(lds_plan + wb * 8 + 4);
+            const int b = __builtin_amdgcn_readfirstlane((int)bs.x) - 1;
+            const uint32_t Q = __builtin_amdgcn_readfirstlane(bs.z);
+            set_priority(b);
+            band_left = b > 0 ? (int)(band_end(Q, b) - band_end(Q, b + 1)) : 0x7FFFFFFF;
+            *(lds_plan + wb * 8 + 4) = (uint32_t)b;
+        }
         if (++k == k1) {                           // the piece ends: store its chunk (rare)
             if (c.live) {
                 const KernArgs kp = kernargs();    // state pointers re-read, not kept live across the loop
@@ -384,7 +444,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             // this wave's index from its job rows' address (kept live across
             // the loop, the index would pin a register)
             const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
-            uint4 pl = *(const uint4*)(lds_plan + wb * 4);
+            uint4 pl = *(const uint4*)(lds_plan + wb * 8);
             pl.x = __builtin_amdgcn_readfirstlane(pl.x);        // one word for the whole wave
             pl.y = __builtin_amdgcn_readfirstlane(pl.y);
             pl.z = __builtin_amdgcn_readfirstlane(pl.z);
@@ -396,7 +456,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             if (++pc == n_pieces(pl)) break;
             const Piece pz = piece_of(pl, pc, nsteps);
             if (pz.wait) wait_head(lds_flag + wb - 1);
-            enter_piece<R, RING>(c, n, pz.chunk);
+            enter_piece<R, RING>(c, n, piece_chunk(pz.chunk));
             k = k0 = pz.k0;
             k1 = pz.k1;
         }
@@ -404,6 +464,19 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
 #ifdef RAFT_PROFILE_PHASES
     if (lane == 0)
         for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
+#endif
+#ifdef RAFT_WAVE_TIMES
+    {
+        const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
+        const int w = blockIdx.x * STEP_WAVES + wib;
+        if (lane == 0 && w < WT_MAX) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);        // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);      // HW_REG_XCC_ID
+            g_wave_times[w][0] = wt0;
+            g_wave_times[w][1] = wt1;
+            g_wave_times[w][2] = ((unsigned long long)xcc << 32) | hw;
+        }
+    }
 #endif
     __syncthreads();
     {   // workgroup partials; the launch's partials geometry re-read from the
@@ -1205,6 +1278,21 @@ int raft_engine_destroy(raft_engine* e) {
             fprintf(stderr, "[phase-cycles]");
             for (int q = 0; q < PH_N; ++q) fprintf(stderr, " %s=%.1f%%", names[q], tot ? 100.0 * v[q] / tot : 0.0);
             fprintf(stderr, " total=%llu\n", tot);
+        }
+    }
+#endif
+#ifdef RAFT_WAVE_TIMES
+    {   // the last step launch's waves: start / end offsets and slots, to stderr
+        (void)hipSetDevice(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        const int nw = std::min(WT_MAX, e->last.workgroups * STEP_WAVES);
+        std::vector<unsigned long long> v((size_t)nw * 3);
+        if (nw > 0 && hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_wave_times), v.size() * 8) == hipSuccess) {
+            unsigned long long t0 = ~0ull;
+            for (int w = 0; w < nw; ++w) t0 = std::min(t0, v[3 * w]);
+            fprintf(stderr, "[wave-times] waves=%d workgroups=%d\n", nw, e->last.workgroups);
+            for (int w = 0; w < nw; ++w)
+                fprintf(stderr, "[wt] %d %llu %llu %llx\n", w, v[3 * w] - t0, v[3 * w + 1] - t0, v[3 * w + 2]);
         }
     }
 #endif
