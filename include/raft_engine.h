@@ -302,7 +302,12 @@ int     raft_engine_reset(raft_engine* e);
 /* Set the index of the next step (its Philox counter c0); with write_state
  * this resumes a run exported at any step. */
 int     raft_engine_set_step_index(raft_engine* e, int64_t t);
-int64_t raft_engine_device_bytes(raft_engine* e); /* HBM owned by the engine */
+/* HBM owned by the engine: the state, logs and counter buffers, plus the
+ * grow-only staging of the handler batches and accessors (kept for the
+ * engine's lifetime at 1.25x the largest request; raft_engine_trim_staging
+ * frees it, page-locked host staging included). */
+int64_t raft_engine_device_bytes(raft_engine* e);
+int     raft_engine_trim_staging(raft_engine* e);
 
 /* ---- state access (fixtures, parity) ----------------------------------- */
 /* out: [n][raft_group_words(R)] int32, canonical layout above. */

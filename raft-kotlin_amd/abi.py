@@ -248,6 +248,7 @@ def load_library(path: str | None = None):
         "raft_engine_wait_stream": (C.c_int, [eng, C.c_void_p]),
         "raft_engine_set_kernel": (C.c_int, [eng, I32]),
         "raft_engine_reset": (C.c_int, [eng]),
+        "raft_engine_trim_staging": (C.c_int, [eng]),
         "raft_engine_device_bytes": (I64, [eng]),
         "raft_engine_read_state": (C.c_int, [eng, I64, I64, P(I32)]),
         "raft_engine_write_state": (C.c_int, [eng, I64, I64, P(I32)]),
@@ -298,7 +299,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
     "raft_engine_set_subranges", "raft_engine_subranges", "raft_engine_kernel_info", "raft_engine_wait_stream",
-    "raft_engine_set_kernel", "raft_engine_reset",
+    "raft_engine_set_kernel", "raft_engine_reset", "raft_engine_trim_staging",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",

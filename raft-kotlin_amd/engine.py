@@ -111,7 +111,12 @@ class RaftEngine:
 
     @property
     def device_bytes(self) -> int:
+        """HBM owned by the engine, the batch / accessor staging included."""
         return int(self._lib.raft_engine_device_bytes(self._h))
+
+    def trim_staging(self):
+        """Free the grow-only staging of the handler batches and accessors."""
+        self._check(self._lib.raft_engine_trim_staging(self._h), "trim_staging")
 
     # -- the hot path -----------------------------------------------------
     def step(self, n: int = 1, counters: bool = True) -> np.ndarray | None:

@@ -735,6 +735,12 @@ def test_device_batches_match_host_batches():
     with pytest.raises(RuntimeError):
         a.vote_batch(bad_g, dst, vq)
     assert np.array_equal(a.read_state(), sa) and a.digest() == b.digest()
+    # the batch staging is engine memory: counted, and freed by trim_staging
+    # (later batches grow it again and give the same results)
+    before = b.device_bytes
+    b.trim_staging()
+    assert b.device_bytes < before
+    assert np.array_equal(b.vote_batch(grp, dst, vq), a.vote_batch(grp, dst, vq))
 
 
 def test_service_wire_path_matches_batches():
