@@ -106,7 +106,7 @@ typedef struct raft_params {
     int32_t  cmd_mode;          /* RAFT_CMD_*                                                       */
     int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
     int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch, 0..RAFT_MAX_STEPS_PER_LAUNCH (0 = 1);
-                                   results never depend on it; <= 431 lets the 7-wave kernels (R <= 5, and
+                                   results never depend on it; <= 429 lets the 7-wave kernels (R <= 5, and
                                    R = 7 without drops) run 7 workgroups per CU (LDS), longer launches run 6 */
     int32_t  mode;              /* RAFT_MODE_* (0 = the reference)                                  */
     int32_t  log_window;        /* 0 = every physical slot is kept (log_cap slots per replica);

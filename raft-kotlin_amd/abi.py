@@ -47,7 +47,7 @@ MAX_STEPS_PER_LAUNCH = 512
 # bench.py's launch length for the step kernels built for 7 waves per SIMD
 # (R <= 5, or R = 7 without drops; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
 # the longest that keeps 7 step workgroups per CU within the LDS (STEP_K_7WG,
-# 431 steps).  The other kernels run 6 workgroups per CU at any length and
+# 429 steps).  The other kernels run 6 workgroups per CU at any length and
 # take the longest launch.
 BENCH_STEPS_PER_LAUNCH = 400
 

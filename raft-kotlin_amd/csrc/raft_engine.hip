@@ -58,7 +58,7 @@ constexpr int STEP_WAVES = STEP_BLOCK / 64;
 constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
 constexpr int TALLY_LDS_WORDS = STEP_WAVES * 16;          // per-wave vote-tally words (Ctx::tl, R >= 4)
 constexpr int FLAG_LDS_WORDS = STEP_WAVES;                // balanced schedule: a wave's head piece is stored
-constexpr int PLAN_LDS_WORDS = STEP_WAVES * 8 + STEP_WAVES;   // each wave's plan (plan_of), priority bands, work left
+constexpr int PLAN_LDS_WORDS = STEP_WAVES * 8;            // each wave's plan (plan_of) and priority band
 constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS + FLAG_LDS_WORDS + PLAN_LDS_WORDS;
 // the longest launch whose LDS (job rows, tally words, K counter rows) still
 // lets 7 step workgroups share a CU's 160 KB
@@ -279,15 +279,6 @@ __device__ __forceinline__ uint32_t plan_units(uint4 pl, int K) {
 }
 // chunk-steps from the start of the wave's quarter to the end of band b (b =
 // 3, 2, 1), per mille of its work (tuning builds set other ends)
-// RAFT_PRIO_MODE 1: the bands below; 2 (tuning builds): every RAFT_PRIO_EVERY
-// steps a wave takes priority 3 - (the number of its workgroup's waves with
-// more chunk-steps left than it), from LDS words each wave updates
-#ifndef RAFT_PRIO_MODE
-#define RAFT_PRIO_MODE 1
-#endif
-#ifndef RAFT_PRIO_EVERY
-#define RAFT_PRIO_EVERY 4
-#endif
 #ifndef RAFT_BAND_ENDS
 #define RAFT_BAND_ENDS 500, 750, 900
 #endif
@@ -385,12 +376,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         const uint32_t Q = plan_units(pl, nsteps);
         // [4]: the band now, [5]: chunk-steps done at its start, [6]: Q
         *(uint4*)(lds_plan + wib * 8 + 4) = make_uint4(3u, 0u, Q, 0u);
-#if RAFT_PRIO_MODE == 2
-        lds_plan[STEP_WAVES * 8 + wib] = Q;        // chunk-steps left (re-ranked every RAFT_PRIO_EVERY)
-        band_left = bal ? RAFT_PRIO_EVERY : 0x7FFFFFFF;
-#else
         band_left = bal ? (int)band_end(Q, 3) : 0x7FFFFFFF;
-#endif
         if (bal) set_priority(3);
         const Piece pz = piece_of(pl, 0, nsteps);
         enter_piece<R, RING>(c, n, piece_chunk(pz.chunk));
@@ -439,19 +425,6 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         if (ib((1ull << NCW) - 1))
             __hip_atomic_fetch_add(&lds_cnt[k * NCW + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         c.clk.mark(PH_CNT);
-#if RAFT_PRIO_MODE == 2
-        if (RARE(--band_left == 0)) {              // re-rank this wave in its workgroup (balanced)
-            const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
-            uint32_t* const left = lds_plan + STEP_WAVES * 8;
-            const uint32_t mine = __builtin_amdgcn_readfirstlane(left[wb]) - RAFT_PRIO_EVERY;
-            left[wb] = mine;
-            const uint4 all = *(const uint4*)left;
-            const int behind = (__builtin_amdgcn_readfirstlane(all.x) < mine) + (__builtin_amdgcn_readfirstlane(all.y) < mine) +
-                               (__builtin_amdgcn_readfirstlane(all.z) < mine) + (__builtin_amdgcn_readfirstlane(all.w) < mine);
-            set_priority(behind);               // the waves with less left than this one
-            band_left = RAFT_PRIO_EVERY;
-        }
-#else
         if (RARE(--band_left == 0)) {              // this wave's next priority band (balanced)
             const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
             uint4 bs = *(const uint4*)(lds_plan + wb * 8 + 4);
@@ -461,7 +434,6 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             band_left = b > 0 ? (int)(band_end(Q, b) - band_end(Q, b + 1)) : 0x7FFFFFFF;
             *(lds_plan + wb * 8 + 4) = (uint32_t)b;
         }
-#endif
         if (++k == k1) {                           // the piece ends: store its chunk (rare)
             if (c.live) {
                 const KernArgs kp = kernargs();    // state pointers re-read, not kept live across the loop

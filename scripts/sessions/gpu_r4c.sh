@@ -9,6 +9,7 @@ OUT=gpurun_out/${TAG:-r4c}; mkdir -p $OUT
 TAG=r4c_d20 ARGS="--steps 20 --warmup 5" bash scripts/pmc_bench.sh; rc=$?; echo "pmc_d20 rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
 TAG=r4c_def ARGS="" bash scripts/pmc_bench.sh; rc=$?; echo "pmc_def rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
 TAG=r4c bash scripts/pmc_handler.sh > $OUT/pmch.log 2>&1; rc=$?; echo "pmch rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
+TAG=r4c bash scripts/phase_budget.sh; rc=$?; echo "phase rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
 for g in 125000 250000 500000; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_s$g" -o run --output-format csv -- \
       python bench.py --steps 20 --warmup 5 --groups $g --no-cpu-baseline --handler-batch 0 --stream-steps 0 \
