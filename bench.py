@@ -578,14 +578,20 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     for ci, (done, k) in enumerate(plan):
         eng.step_async(k, rows[ci])
         if coll:
-            # the only collective: the batched per-step counter all-reduce,
-            # off the critical path on a side stream (counters never feed
-            # back); this rank's own rows stay in `counters`
+            # the only collective: the batched per-step counter all-reduce on
+            # a side stream (counters never feed back); this rank's own rows
+            # stay in `counters`.  The next launch waits for it: a balanced
+            # launch holds exactly the workgroups the GPU keeps resident, so
+            # an RCCL kernel running beside it displaces some of them into a
+            # second round (1.9e10 -> 1.3e10 group-steps/s at one rank,
+            # DESIGN.md §6); in series it costs one all-reduce per chunk
             chunk_ev[ci].record(stream)
             comm_stream.wait_event(chunk_ev[ci])
             with torch.cuda.stream(comm_stream):
                 gcounters[done:done + k].copy_(counters[done:done + k])
                 dist.all_reduce(gcounters[done:done + k])
+            if done + k < args.steps:
+                eng.wait_stream(comm_stream.cuda_stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
     wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
@@ -843,6 +849,12 @@ def main(argv=None, result=None):
                     "s_waitcnt/barrier, SQ_WAIT_INST_ANY ready but not issued; MI355X_MICROARCH.md SQ block)",
         }
 
+    # ---- the general kernel (untimed for `value`): the warmup and timed legs
+    # replayed from step 0, ending at the same state ----
+    general = None
+    if world == 1 and not coll and not args.no_general_leg and net != abi.NET_ALL:
+        general = general_kernel_leg(eng, args, chunk, dev, c_loc, kern_avg_ms)
+
     # ---- streaming leg (untimed for `value`): one step per launch, so every
     # launch streams the whole group state HBM -> VGPRs -> HBM.  Its roofline
     # is the HBM-bound formulation of the same step. ----
@@ -874,18 +886,14 @@ def main(argv=None, result=None):
                      "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
-    general = None
-    if world == 1 and not coll and not args.no_general_leg and net != abi.NET_ALL:
-        general = general_kernel_leg(eng, args, chunk, dev, c_loc, kern_avg_ms)
-
     if args.plan_file and rank == 0:
         # [leg, steps, dispatches]: a launch of the warmup / timed legs is one
         # step-kernel dispatch per sub-range; the streaming leg runs one range
         seq = [["warmup", x, nsub] for x in launch_plan(args.warmup, L)] + [["timed", x, nsub] for x in timed_plan]
-        seq += [["streaming", 1, 1]] * args.stream_steps
         if general is not None:                   # the general kernel replays the warmup and timed launches
             seq += [["general_warmup", x, nsub] for x in launch_plan(args.warmup, L)]
             seq += [["general", x, nsub] for x in timed_plan]
+        seq += [["streaming", 1, 1]] * args.stream_steps
         json.dump({"key": pmc_key, "stream_steps": args.stream_steps, "R": R, "launches": seq},
                   open(args.plan_file, "w"))
 

@@ -280,6 +280,11 @@ struct PhaseClock {
         acc[k] += now - last;
         last = now;
     }
+#elif defined(RAFT_PHASE_MARKS)
+    // ISA inspection builds: an assembly comment at each phase end
+    __device__ __forceinline__ void start() {}
+    template <class I>
+    __device__ __forceinline__ void mark(I k) { asm volatile(";@PHASE_END %0" ::"i"((int)k)); }
 #else
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}

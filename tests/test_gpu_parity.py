@@ -276,7 +276,7 @@ BALANCED_CASES = [(1, 20, 1), (3, 7, 1), (7, 37, 1), (7, 400, 1), (50, 20, 1), (
 @pytest.mark.parametrize("cfg", ["c3", "c5", "c2"])
 @pytest.mark.parametrize("case", BALANCED_CASES, ids=[f"wg{a}-k{b}-sub{c}" for a, b, c in BALANCED_CASES])
 def test_balanced_schedule_vs_oracle(oracle_runs, cfg, case):
-    """The balanced schedule (raft_params.schedule, DESIGN.md §4.3): a
+    """The balanced schedule (raft_params.schedule, DESIGN.md §4.4): a
     workgroup's waves split its chunks' chunk-steps, a chunk passing from one
     wave to the next between two steps through HBM and an in-workgroup LDS
     flag.  Every per-step counter and the whole-run digest equal the oracle's
