@@ -40,6 +40,23 @@ def kernels(d, counter=None):
     return [(k, name[k], acc[k]) for k in sorted(acc)]
 
 
+def short(nm):
+    """A kernel's name without namespaces, template arguments or parameters."""
+    nm = nm.replace("(anonymous namespace)::", "").split("(")[0]
+    return nm.split("<")[0].split("::")[-1].replace("void ", "").strip()
+
+
+def runs(names):
+    """Consecutive repeats folded: ["a", "b", "b"] -> ["a", "b x2"]."""
+    out = []
+    for nm in names:
+        if out and out[-1][0] == nm:
+            out[-1][1] += 1
+        else:
+            out.append([nm, 1])
+    return [nm if c == 1 else f"{nm} x{c}" for nm, c in out]
+
+
 def batches(rows):
     """Group a dispatch list into handler batches: each starts at a batch_keys_kernel."""
     out, cur = [], None
@@ -81,7 +98,7 @@ def main(d):
                      "handler_kernel_fetch_bytes": hfetch, "handler_kernel_write_bytes": hwrite,
                      "kernels_ms_per_batch": t_all, "handler_kernel_ms": t_h,
                      "handler_kernel_hbm_gbs": (hfetch + hwrite) / (t_h / 1e3) / 1e9 if t_h else None,
-                     "kernels_per_batch": [nm.split("(")[0][-60:] for nm, _ in tb[ix[0]]],
+                     "kernels_per_batch": runs([short(nm) for nm, _ in tb[ix[0]]]),
                      "fetch_factor": ff, "write_factor": wf,
                      "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes + --kernel-trace "
                                f"(scripts/pmc_handler.sh, {os.path.basename(d)})"})

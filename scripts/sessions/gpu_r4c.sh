@@ -6,8 +6,10 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r4c}; mkdir -p $OUT
+# raw rocprofv3 csv files are compressed on the way out (gpurun copies back <= 64 MiB)
+trap 'find gpurun_out -name "*.csv" -size +256k -exec gzip -q {} +' EXIT
 TAG=r4c_d20 ARGS="--steps 20 --warmup 5" bash scripts/pmc_bench.sh; rc=$?; echo "pmc_d20 rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
-TAG=r4c_def ARGS="" bash scripts/pmc_bench.sh; rc=$?; echo "pmc_def rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
+TAG=r4c_def ARGS="--handler-batch 0" bash scripts/pmc_bench.sh; rc=$?; echo "pmc_def rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
 TAG=r4c bash scripts/pmc_handler.sh > $OUT/pmch.log 2>&1; rc=$?; echo "pmch rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
 TAG=r4c bash scripts/phase_budget.sh; rc=$?; echo "phase rc=$rc" >> $OUT/status.txt; [ $rc -eq 0 ] || exit $rc
 for g in 125000 250000 500000; do

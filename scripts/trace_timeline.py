@@ -16,7 +16,7 @@ def main(d):
     rows = []
     for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row["Kernel_Name"].split("(")[0][-70:]))
+            rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-70:]))
     rows.sort()
     steps = [i for i, r in enumerate(rows) if "step_kernel" in r[2]]
     if not steps:
