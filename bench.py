@@ -22,7 +22,8 @@ line then also carries `weak_scaling`, measured in the same job: every GPU its
 own 10^6 groups, timed the same way, whose rank-0 counter rows must equal the
 strong leg's all-reduced rows (the same global groups).  --scaling weak swaps
 the two (the strong leg is then `config4_strong`).  The only collective is the
-all-reduce of the per-step counter rows over RCCL, batched on a side stream.
+all-reduce of the per-step counter rows over RCCL, once the clock has stopped
+(--allreduce inline: per chunk inside the timed region, in series).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -281,7 +282,11 @@ def parse_args(argv=None):
                     help="ring slots per replica (power of two; 0 = keep every physical slot); default: every slot "
                          "while that fits 60%% of HBM, else 256 for configs 2 and 3 (DESIGN.md §4.2)")
     ap.add_argument("--reduce-every", type=int, default=512,
-                    help="steps per counter all-reduce (rounded to whole launches)")
+                    help="steps per step_async call and per inline counter all-reduce (rounded to whole launches)")
+    ap.add_argument("--allreduce", choices=["after", "inline"], default="after",
+                    help="N > 1: all-reduce the per-step counter rows once after the timed region (they are "
+                         "observations, not the data path), or per --reduce-every chunk inside it, in series "
+                         "with the launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-general-leg", action="store_true",
                     help="N = 1: skip the general_kernel leg (the main leg on the run-time-decided kernel)")
@@ -527,9 +532,10 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
 
 def timed_leg(eng, args, chunk, coll, dev, world):
     """Warmup (untimed), then the timed region of `args.steps` lockstep steps on
-    `eng`: enqueued in chunks of `chunk` steps, each chunk's counter rows
-    all-reduced on a side stream when `coll`, bracketed by a barrier and a
-    device sync on both sides.  Returns this rank's clock, the stream-event and
+    `eng`: enqueued in chunks of `chunk` steps, bracketed by a barrier and a
+    device sync on both sides; when `coll`, the counter rows all-reduced over
+    the ranks after the clock stops (--allreduce after) or per chunk in series
+    with the launches (inline).  Returns this rank's clock, the stream-event and
     step-kernel times, the job's elapsed time (MAX over ranks) and the counter
     rows (this rank's, all ranks', warmup)."""
     import torch
@@ -569,7 +575,8 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     # launch, 6 % of the driver's 20-step run)
     plan = [(q, min(chunk, args.steps - q)) for q in range(0, args.steps, chunk)]
     rows = [counters[q].data_ptr() for q, _ in plan]
-    chunk_ev = [torch.cuda.Event() for _ in plan] if coll else []
+    inline = coll and args.allreduce == "inline"
+    chunk_ev = [torch.cuda.Event() for _ in plan] if inline else []
     torch.cuda.synchronize(dev)
     if coll:
         dist.barrier()
@@ -577,14 +584,13 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     ev0.record(stream)
     for ci, (done, k) in enumerate(plan):
         eng.step_async(k, rows[ci])
-        if coll:
-            # the only collective: the batched per-step counter all-reduce on
-            # a side stream (counters never feed back); this rank's own rows
-            # stay in `counters`.  The next launch waits for it: a balanced
-            # launch holds exactly the workgroups the GPU keeps resident, so
-            # an RCCL kernel running beside it displaces some of them into a
-            # second round (1.9e10 -> 1.3e10 group-steps/s at one rank,
-            # DESIGN.md §6); in series it costs one all-reduce per chunk
+        if inline:
+            # --allreduce inline: the per-step counter rows all-reduced per
+            # chunk on a side stream, the next launch waiting for it: a
+            # balanced launch holds exactly the workgroups the GPU keeps
+            # resident, so an RCCL kernel running beside it displaces some of
+            # them into a second round (1.9e10 -> 1.3e10 group-steps/s at one
+            # rank)
             chunk_ev[ci].record(stream)
             comm_stream.wait_event(chunk_ev[ci])
             with torch.cuda.stream(comm_stream):
@@ -597,6 +603,13 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
     if coll:
         dist.barrier()
+        if not inline:
+            # the counter rows of every rank, summed once the clock has
+            # stopped: the only collective, and off the data path (the
+            # groups never exchange anything)
+            gcounters.copy_(counters)
+            dist.all_reduce(gcounters)
+            torch.cuda.synchronize(dev)
     ev_ms = ev0.elapsed_time(ev1)
     kern_ms, launches = eng.kernel_time()
     eng.set_kernel_timing(False)
@@ -743,8 +756,8 @@ def main(argv=None, result=None):
     # RAFT_BENCH_BACKEND=gloo with RAFT_BENCH_ONE_DEVICE=1 runs every rank on
     # cuda:0 with gloo collectives, which exercises the N > 1 path end to end
     # RAFT_BENCH_FORCE_COLLECTIVE=1 runs the collective branch at WORLD_SIZE 1:
-    # a one-rank communicator (RCCL by default), the side-stream counter
-    # all-reduce per chunk and the elapsed / kernel-time reductions, so the
+    # a one-rank communicator (RCCL by default), the counter
+    # all-reduce and the elapsed / kernel-time reductions, so the
     # multi-GPU path executes on a one-GPU box (tests/test_gpu_bench.py)
     backend = os.environ.get("RAFT_BENCH_BACKEND", "nccl")
     if os.environ.get("RAFT_BENCH_ONE_DEVICE") == "1":
@@ -955,7 +968,7 @@ def main(argv=None, result=None):
             "subranges": nsub,
             "step_waves_per_rank": -(-G_local // (64 // R)),
             "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window, net) < abi.MAX_STEPS_PER_LAUNCH),
-            "counter_allreduce_every": chunk if coll else None,
+            "counter_allreduce_every": (chunk if args.allreduce == "inline" else "after_timed_region") if coll else None,
             "collective": ({"backend": backend, "ranks": world, "forced_at_one_rank": world == 1} if coll else None),
         },
         "roofline": {

@@ -3,9 +3,9 @@
 The driver runs config 4 (10^6 x 5 sharded over 2/4/8 GPUs) with one RCCL
 communicator per node; a one-GPU box can still execute every line of that
 branch at WORLD_SIZE 1 (RAFT_BENCH_FORCE_COLLECTIVE=1): the `nccl` (RCCL)
-process group created with device_id, the per-chunk copy + all_reduce of the
-counter rows on a side stream ordered after the step launches by events,
-and the MAX / all-gather reductions of the elapsed and kernel times.  The
+process group created with device_id, the all_reduce of the counter rows
+after the timed region (or per chunk on a side stream, in series with the
+launches: --allreduce inline), and the MAX / all-gather reductions of the elapsed and kernel times.  The
 all-reduced rows must equal this rank's own rows and the CPU oracle's
 counters for the same global groups and steps.  bench.main runs in this
 process (no child process once the GPU is initialised).
@@ -27,8 +27,8 @@ bench = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(bench)
 
 
-@pytest.mark.parametrize("backend", ["nccl", "gloo"])
-def test_forced_collective_at_one_rank(backend, monkeypatch):
+@pytest.mark.parametrize("backend,mode", [("nccl", "after"), ("nccl", "inline"), ("gloo", "after")])
+def test_forced_collective_at_one_rank(backend, mode, monkeypatch):
     monkeypatch.setenv("RAFT_BENCH_FORCE_COLLECTIVE", "1")
     monkeypatch.setenv("RAFT_BENCH_BACKEND", backend)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
@@ -36,11 +36,11 @@ def test_forced_collective_at_one_rank(backend, monkeypatch):
     G, warm, steps = 24_000, 40, 800          # two 400-step launches: two all-reduce chunks at --reduce-every 400
     res = {}
     rc = bench.main(["--groups", str(G), "--steps", str(steps), "--warmup", str(warm), "--stream-steps", "0",
-                     "--reduce-every", "400", "--no-cpu-baseline"], result=res)
+                     "--reduce-every", "400", "--allreduce", mode, "--no-cpu-baseline"], result=res)
     assert rc == 0
     out = res["out"]
     assert out["config"]["collective"] == {"backend": backend, "ranks": 1, "forced_at_one_rank": True}
-    assert out["config"]["counter_allreduce_every"] == 400
+    assert out["config"]["counter_allreduce_every"] == (400 if mode == "inline" else "after_timed_region")
     assert out["valid"] and out["value"] > 0
     ca, cl = res["counters_all"], res["counters_local"]
     assert np.array_equal(ca, cl), "a one-rank all-reduce must return this rank's rows"
