@@ -8,7 +8,7 @@
 // handlers read or write, and (rarely) non-primary session rows.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -789,30 +789,32 @@ struct BatchCounters {
 // next to each other in batch order, and batch_kernel runs one thread per
 // sorted position: the first position of each key's run loads that replica,
 // applies the run's messages in order and stores it back.
+// Key: uint32_t while G * R fits (half the sort's key traffic), else uint64_t.
+template <class Key>
 __global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __restrict__ group,
                                                            const int32_t* __restrict__ dst, int n, int64_t G, int R,
-                                                           uint64_t* __restrict__ keys, uint32_t* __restrict__ ord,
+                                                           Key* __restrict__ keys, uint32_t* __restrict__ ord,
                                                            unsigned int* flags) {
     const int m = blockIdx.x * BLOCK + threadIdx.x;
     if (m >= n) return;
     const int64_t g = group[m];
     const int32_t d = dst[m];
     const bool ok = g >= 0 && g < G && d >= 0 && d < R;
-    keys[m] = ok ? (uint64_t)g * (uint64_t)R + (uint64_t)d : 0ull;
+    keys[m] = ok ? (Key)((uint64_t)g * (uint64_t)R + (uint64_t)d) : (Key)0;
     ord[m] = (uint32_t)m;
     if (!ok) atomicOr(&flags[0], 1u);
 }
 
 // flags[0]: a message was outside the engine (nothing is applied);
 // flags[1]: accesses below the retained log window (RAFT_EWINDOW)
-template <bool TB>
+template <bool TB, class Key>
 __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int n,
-                                                      const uint64_t* __restrict__ keys,
+                                                      const Key* __restrict__ keys,
                                                       const uint32_t* __restrict__ order, const void* req, void* resp,
                                                       unsigned int* flags) {
     const int m0 = blockIdx.x * BLOCK + threadIdx.x;
     if (m0 >= n || *(volatile unsigned int*)&flags[0]) return;
-    const uint64_t key = keys[m0];
+    const Key key = keys[m0];
     if (m0 > 0 && keys[m0 - 1] == key) return;                          // not the first of its run
     const int R = p.R;
     const int64_t idx = (int64_t)key;
@@ -1731,36 +1733,54 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
 }
 
 
-// The batch on device buffers: keys, a stable radix sort over the key bits,
-// the handlers; one synchronisation at the end for the status flags.
-static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
-                         void* resp, int64_t n64) {
-    e->fork_needed = true;
-    const int n = (int)n64;
+// rocprim's radix sort takes its merge-sort path up to 2^20 items (one
+// block sort and ~10 merge passes over the whole array, 21 dispatches at 10^6
+// messages); a merge limit of 0 keeps it on the onesweep path (a histogram
+// pass and one pass per 8 key bits).
+using BatchSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                   rocprim::default_config, 0>;
+extern "C++" template <class Key>
+static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                          void* resp, int n, int bits) {
     const int R = e->p.R;
-    int bits = 1;
-    while (bits < 64 && ((uint64_t)e->p.G * (uint64_t)R - 1) >> bits) ++bits;
     size_t sort_tmp = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                               (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0, bits, e->stream));
-    const size_t b_keys = al256((size_t)n * 8), b_ord = al256((size_t)n * 4);
+    HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(nullptr, sort_tmp, (const Key*)nullptr, (Key*)nullptr,
+                                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u,
+                                                       (unsigned)bits, e->stream));
+    const size_t b_keys = al256((size_t)n * sizeof(Key)), b_ord = al256((size_t)n * 4);
     if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, 2 * b_keys + 2 * b_ord + al256(sort_tmp) + 256)) return rc;
     char* b = e->bst;
-    uint64_t* k_in = (uint64_t*)b; b += b_keys;
-    uint64_t* k_out = (uint64_t*)b; b += b_keys;
+    Key* k_in = (Key*)b; b += b_keys;
+    Key* k_out = (Key*)b; b += b_keys;
     uint32_t* o_in = (uint32_t*)b; b += b_ord;
     uint32_t* o_out = (uint32_t*)b; b += b_ord;
     unsigned int* flags = (unsigned int*)b; b += 256;
     void* tmp = b;
     HIP_TRY(hipMemsetAsync(flags, 0, 8, e->stream));
     const unsigned grid = (unsigned)((n + BLOCK - 1) / BLOCK);
-    batch_keys_kernel<<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, k_in, o_in, flags);
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, sort_tmp, k_in, k_out, o_in, o_out, n, 0, bits, e->stream));
-    auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true> : batch_kernel<false>;
+    batch_keys_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, k_in, o_in, flags);
+    HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(tmp, sort_tmp, k_in, k_out, o_in, o_out, n, 0u, (unsigned)bits,
+                                                       e->stream));
+    auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true, Key> : batch_kernel<false, Key>;
     kern<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, kind, n, k_out, o_out, req, resp, flags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    return RAFT_OK;
+}
+
+// The batch on device buffers: keys, a stable radix sort over the key bits,
+// the handlers; one synchronisation at the end for the status flags.
+static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                         void* resp, int64_t n64) {
+    e->fork_needed = true;
+    const int n = (int)n64;
+    const uint64_t nkeys = (uint64_t)e->p.G * (uint64_t)e->p.R;
+    int bits = 1;
+    while (bits < 64 && (nkeys - 1) >> bits) ++bits;
+    const int rc = bits <= 32 ? run_batch_keys<uint32_t>(e, kind, group, dst, req, resp, n, bits)
+                              : run_batch_keys<uint64_t>(e, kind, group, dst, req, resp, n, bits);
+    if (rc) return rc;
     e->cache_valid = false;
     if (e->bflags_host[0]) return fail(RAFT_ERANGE, "a message's group or replica index is outside the engine; "
                                                     "nothing was applied");
