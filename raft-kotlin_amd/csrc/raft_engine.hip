@@ -737,36 +737,57 @@ struct RepState {
     __device__ Rep ref() { return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl, t1, t2, c1}; }
 };
 
+// VOTE_ONLY: the fields vote() and the timer re-arm touch (RaftServer.kt:228-251)
+// -- the others are neither read nor written back
+template <bool VOTE_ONLY = false>
 __device__ __forceinline__ void load_rep(RepState& x, const DevParams& p, int64_t idx) {
 #define LD(f) p.st[fidx(p, f, idx)]
-    x.term = LD(RAFT_F_TERM); x.voted = LD(RAFT_F_VOTED); x.role = LD(RAFT_F_ROLE); x.commit = LD(RAFT_F_COMMIT);
-    x.last = LD(RAFT_F_LAST); x.phys = LD(RAFT_F_PHYS); x.elec = LD(RAFT_F_ELECTION_MS);
-    x.fl = (uint32_t)LD(RAFT_F_FLAGS); x.phase = LD(RAFT_F_PHASE_MS); x.retry = LD(RAFT_F_RETRY_MS);
+    x.term = LD(RAFT_F_TERM); x.voted = LD(RAFT_F_VOTED); x.role = LD(RAFT_F_ROLE);
+    x.last = LD(RAFT_F_LAST); x.phys = LD(RAFT_F_PHYS); x.fl = (uint32_t)LD(RAFT_F_FLAGS);
+    if (VOTE_ONLY) {
+        x.commit = x.elec = x.phase = x.retry = 0;
+    } else {
+        x.commit = LD(RAFT_F_COMMIT); x.elec = LD(RAFT_F_ELECTION_MS);
+        x.phase = LD(RAFT_F_PHASE_MS); x.retry = LD(RAFT_F_RETRY_MS);
+    }
 #undef LD
 }
 
-// the batch path derives the tail cache from the log (the HBM copy may be stale)
+// the batch path derives the tail cache from the log (the HBM copy may be
+// stale); vote() reads only the last entry's term
+template <bool VOTE_ONLY = false>
 __device__ __forceinline__ void derive_cache(RepState& x, const LogView& lv) {
     const uint2 a = x.last >= 1 ? *lv.at(x.last - 1) : make_uint2(0u, 0u);
     x.t1 = (int32_t)a.x;
     x.c1 = a.y;
-    x.t2 = x.last >= 2 ? (int32_t)lv.at(x.last - 2)->x : 0;
+    x.t2 = !VOTE_ONLY && x.last >= 2 ? (int32_t)lv.at(x.last - 2)->x : 0;
 }
 
-__device__ __forceinline__ void store_rep(const RepState& x, const DevParams& p, int64_t idx) {
-#define ST(f) p.st[fidx(p, f, idx)]
-    ST(RAFT_F_TERM) = x.term; ST(RAFT_F_VOTED) = x.voted; ST(RAFT_F_ROLE) = x.role; ST(RAFT_F_COMMIT) = x.commit;
-    ST(RAFT_F_LAST) = x.last; ST(RAFT_F_PHYS) = x.phys; ST(RAFT_F_ELECTION_MS) = x.elec;
-    ST(RAFT_F_FLAGS) = (int32_t)(x.fl & FL_EXPORT_MASK); ST(RAFT_F_PHASE_MS) = x.phase; ST(RAFT_F_RETRY_MS) = x.retry;
+// Only the fields that changed are written back: a random replica's field is
+// a 32-B sector of its own, so an unchanged field would cost a sector write.
+// drew: the timer was re-armed (resolve_rep_draw wrote elec).
+template <bool VOTE_ONLY = false>
+__device__ __forceinline__ void store_rep(const RepState& x, const RepState& o, bool drew, const DevParams& p,
+                                          int64_t idx) {
+#define ST(f, v, w) if ((v) != (w)) p.st[fidx(p, f, idx)] = (v)
+    ST(RAFT_F_TERM, x.term, o.term); ST(RAFT_F_VOTED, x.voted, o.voted); ST(RAFT_F_ROLE, x.role, o.role);
+    ST(RAFT_F_FLAGS, (int32_t)(x.fl & FL_EXPORT_MASK), (int32_t)(o.fl & FL_EXPORT_MASK));
+    if (drew || (!VOTE_ONLY && x.elec != o.elec)) p.st[fidx(p, RAFT_F_ELECTION_MS, idx)] = x.elec;
+    if (!VOTE_ONLY) {
+        ST(RAFT_F_COMMIT, x.commit, o.commit); ST(RAFT_F_LAST, x.last, o.last); ST(RAFT_F_PHYS, x.phys, o.phys);
+        ST(RAFT_F_PHASE_MS, x.phase, o.phase); ST(RAFT_F_RETRY_MS, x.retry, o.retry);
+    }
 #undef ST
 }
 
-__device__ __forceinline__ void resolve_rep_draw(RepState& x, const DevParams& p, uint32_t t, uint32_t gid, int r) {
+__device__ __forceinline__ bool resolve_rep_draw(RepState& x, const DevParams& p, uint32_t t, uint32_t gid, int r) {
     if (x.fl & FL_DRAW) {
         const u32x4 w = draw(p, t, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
         x.elec = scale_range(word_of(w, r & 3), p.emin, p.emax);
         x.fl &= ~FL_DRAW;
+        return true;
     }
+    return false;
 }
 
 enum { BATCH_VOTE = 0, BATCH_APPEND = 1, BATCH_COMMAND = 2 };
@@ -807,8 +828,8 @@ __global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __rest
 
 // flags[0]: a message was outside the engine (nothing is applied);
 // flags[1]: accesses below the retained log window (RAFT_EWINDOW)
-template <bool TB, class Key>
-__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int kind, int n,
+template <bool TB, class Key, int kind>
+__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int n,
                                                       const Key* __restrict__ keys,
                                                       const uint32_t* __restrict__ order, const void* req, void* resp,
                                                       unsigned int* flags) {
@@ -821,14 +842,17 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
     const int64_t i = idx / R;
     const int r = (int)(idx - i * R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
+    constexpr bool VO = kind == BATCH_VOTE;
     RepState x;
-    load_rep(x, p, idx);
+    load_rep<VO>(x, p, idx);
+    const RepState o = x;
     const LogView lv = log_of(p, idx);
-    derive_cache(x, lv);
+    derive_cache<VO>(x, lv);
     BatchCounters cnt;
+    bool drew = false;
     for (int m = m0; m < n && keys[m] == key; ++m) {
         const uint32_t o = order[m];
-        if (kind == BATCH_VOTE) {
+        if constexpr (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
             uint64_t gr;
@@ -836,7 +860,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
                                    __ballot(x.phys - x.last >= p.W), __ballot(x.last >= 1), follower_sent(x.fl), cnt,
                                    rt, gr);
             ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
-        } else if (kind == BATCH_APPEND) {
+        } else if constexpr (kind == BATCH_APPEND) {
             const raft_append_req q = ((const raft_append_req*)req)[o];
             int32_t rt = 0;
             uint64_t su = 0, st = 0;
@@ -853,9 +877,9 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
         } else {
             append_command<TB, true>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);
         }
-        resolve_rep_draw(x, p, t, gid, r);
+        drew |= resolve_rep_draw(x, p, t, gid, r);
     }
-    store_rep(x, p, idx);
+    store_rep<VO>(x, o, drew, p, idx);
     if (cnt.miss) atomicAdd(&flags[1], cnt.miss);
 }
 
@@ -1761,8 +1785,12 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
     batch_keys_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, k_in, o_in, flags);
     HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(tmp, sort_tmp, k_in, k_out, o_in, o_out, n, 0u, (unsigned)bits,
                                                        e->stream));
-    auto* kern = e->p.mode == RAFT_MODE_TEXTBOOK ? batch_kernel<true, Key> : batch_kernel<false, Key>;
-    kern<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, kind, n, k_out, o_out, req, resp, flags);
+    using BK = void (*)(DevParams, uint32_t, int, const Key*, const uint32_t*, const void*, void*, unsigned int*);
+    const bool tb = e->p.mode == RAFT_MODE_TEXTBOOK;
+    BK kern = kind == BATCH_VOTE     ? (tb ? batch_kernel<true, Key, BATCH_VOTE> : batch_kernel<false, Key, BATCH_VOTE>)
+              : kind == BATCH_APPEND ? (tb ? batch_kernel<true, Key, BATCH_APPEND> : batch_kernel<false, Key, BATCH_APPEND>)
+                                     : (tb ? batch_kernel<true, Key, BATCH_COMMAND> : batch_kernel<false, Key, BATCH_COMMAND>);
+    kern<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, k_out, o_out, req, resp, flags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
