@@ -604,12 +604,13 @@ def random_states(rng, n, R, cap):
 
 
 @pytest.mark.parametrize("mode,G,n", [(abi.MODE_REFERENCE, 64, 3000), (abi.MODE_TEXTBOOK, 64, 3000),
-                                      (abi.MODE_REFERENCE, 4000, 100_000)])
+                                      (abi.MODE_REFERENCE, 4000, 100_000), (abi.MODE_REFERENCE, 1, 4000)])
 def test_handler_batches_vs_oracle(mode, G, n):
     """The single-handler batches (RaftServer.vote() / append() /
     appendCommand(), RaftServer.kt:228-287, :100-107) against the oracle's
     handlers message by message: at n = 3000 on 64 groups (long runs of
-    messages per replica) and at n = 10^5 on 4000 groups."""
+    messages per replica), at n = 10^5 on 4000 groups, and 4000 messages to
+    one group (runs of ~800 per replica through the radix sort's passes)."""
     rng = np.random.default_rng(7)
     R, cap = 5, 8
     w, lt, lc = random_states(rng, G, R, cap)
