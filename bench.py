@@ -797,8 +797,8 @@ def main(argv=None, result=None):
     spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window, net)
     L = launch_length(args.steps, spl)                      # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
-    # launch sub-ranges: 0 = the engine's automatic choice (one: the balanced
-    # schedule ends a launch's waves together)
+    # launch sub-ranges: 0 = the engine's automatic choice (one on the balanced
+    # schedule; three for a partitions-only workload)
     subranges = args.subranges
     params = abi.make_params(log_cap=log_cap, log_window=window, steps_per_launch=L, mode=mode, subranges=subranges,
                              schedule=SCHEDULES[args.schedule], schedule_workgroups=args.schedule_workgroups,

@@ -41,7 +41,7 @@ extern "C" {
 #endif
 
 /* 2: raft_params.schedule / schedule_workgroups / kernel, automatic
- * subranges = 1, raft_engine_kernel_info, raft_engine_set_kernel,
+ * subranges by workload (1 or 3), raft_engine_kernel_info, raft_engine_set_kernel,
  * raft_engine_reset, raft_engine_wait_stream */
 #define RAFT_ABI_VERSION 2
 
@@ -124,11 +124,13 @@ typedef struct raft_params {
     int32_t  subranges;         /* engine only: the step kernel's chunks (waves of groups) split into
                                  * this many contiguous ranges, each launched on its own stream, so
                                  * that one range's last waves can overlap another's next launch.
-                                 * 0 = automatic = 1 (ABI 2; ABI 1 chose 3: the balanced schedule
-                                 * below ends every wave of a launch together, so one range is
-                                 * enough), 1..RAFT_MAX_SUBRANGES.  Results never depend on it.    */
-    int32_t  schedule;          /* engine only: RAFT_SCHED_* (0 = automatic).  Results never depend
-                                 * on it.                                                          */
+                                 * 0 = automatic (ABI 2): 1 with the balanced schedule, 3 for a
+                                 * partitions-only workload (configs 5, 2, 1), whose automatic
+                                 * schedule is one chunk per wave; 1..RAFT_MAX_SUBRANGES.  Results
+                                 * never depend on it.                                             */
+    int32_t  schedule;          /* engine only: RAFT_SCHED_* (0 = automatic: balanced when the
+                                 * chunks outnumber the resident wave slots, except for a
+                                 * partitions-only workload).  Results never depend on it.        */
     int32_t  schedule_workgroups; /* engine only: workgroups of a balanced launch (0 = as many as
                                  * the GPU holds at once at the launch's LDS; tests set fewer)     */
     int32_t  kernel;            /* engine only: RAFT_KERNEL_AUTO (0): the step kernel built for the

@@ -925,6 +925,7 @@ struct raft_engine {
     int ncu;                    // compute units of the device
     // the launch schedule (raft_params.schedule, schedule_workgroups; step_kernel)
     int schedule, sched_wg;
+    bool part_only;             // the workload's kernel is partitions-only (auto_subranges)
     raft_kernel_info last;      // the last step launch (raft_engine_kernel_info)
     const void* occ_kern;       // workgroups per CU of occ_kern at occ_lds bytes of LDS (cached)
     size_t occ_lds;
@@ -1060,8 +1061,9 @@ static int launch_geo(raft_engine* e, StepKernel kern, int k, LaunchGeo& geo) {
         const int n = b - a;
         // AUTO: when the chunks outnumber the resident wave slots (of this
         // sub-range's share); BALANCED: whenever a workgroup gets 4 chunks
-        const bool bal = e->schedule == RAFT_SCHED_BALANCED ? n >= STEP_WAVES
-                                                            : e->schedule == RAFT_SCHED_AUTO && n > STEP_WAVES * cap;
+        const bool bal = e->schedule == RAFT_SCHED_BALANCED
+                             ? n >= STEP_WAVES
+                             : e->schedule == RAFT_SCHED_AUTO && !e->part_only && n > STEP_WAVES * cap;
         geo.w0[q] = a;
         geo.w0[q + 1] = b;
         geo.bal[q] = bal ? n : 0;
@@ -1272,6 +1274,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
         *out = nullptr;
         return fail(RAFT_ENOMEM, "hipHostMalloc of the batch status flags failed");
     }
+    e->part_only = step_net(d, *p, p->R, d.churn_thr32 != 0) == NET_PART;
     if (int rc = raft_engine_set_subranges(e, p->subranges)) {
         raft_engine_destroy(e);
         *out = nullptr;
@@ -1512,7 +1515,13 @@ int raft_engine_set_steps_per_launch(raft_engine* e, int32_t k) {
 // with another's next launch: 1.25e5 groups 1.36 -> 1.73e10, 1e6 groups 1.78
 // -> 1.86e10 group-steps/s; the balanced schedule ends a launch's waves
 // together instead, with no side streams)
-constexpr int AUTO_SUBRANGES = 1;
+// The automatic launch shape.  Drops and churn (config 3 and its shards):
+// one range on the balanced schedule.  Partitions alone (configs 5, 2, 1: the
+// partitions-only kernel): one chunk per wave over three overlapping ranges,
+// which measured 3.6 % above the balanced schedule on config 5 (whose
+// partitions make a chunk's work uneven, which equal chunk-steps per wave do
+// not balance) and 23 % above one range (profiles/r4_k).
+static int auto_subranges(const raft_engine* e) { return e->part_only ? 3 : 1; }
 int raft_engine_wait_stream(raft_engine* e, void* stream) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     HIP_TRY(hipSetDevice(e->device));
@@ -1551,7 +1560,7 @@ int raft_engine_kernel_info(raft_engine* e, raft_kernel_info* out) {
 int raft_engine_set_subranges(raft_engine* e, int32_t n) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     if (n < 0 || n > RAFT_MAX_SUBRANGES) return fail(RAFT_EINVAL, "subranges must be 0..RAFT_MAX_SUBRANGES");
-    if (n == 0) n = AUTO_SUBRANGES;
+    if (n == 0) n = auto_subranges(e);
     n = std::min(n, e->nblocks);
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));

@@ -447,26 +447,26 @@ FULL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "full_
 # true> (7 waves as well).  Config 5 is always flat; bench.py launches it at K = 400
 # (the partitions-only R = 7 kernel at 7 waves per SIMD; K = 500 and 512 run
 # it at 6 workgroups per CU).
-# A fourth element is the launch sub-ranges (streams); default: the engine's
-# automatic choice (3, the bench's configuration).
-# A fourth element is the launch sub-ranges (streams; default 1, the engine's
-# automatic choice), a fifth the schedule (default automatic: balanced
-# whenever the chunks outnumber the resident wave slots, which they do at
-# both full sizes).  (3, 0, 20, 1) is the driver's exact timed launch.
-ONE = abi.SCHED_ONE_PER_WAVE
+# A fourth element is the launch sub-ranges (streams; default: the engine's
+# automatic choice, 1 for config 3 and 3 for config 5), a fifth the schedule
+# (default automatic: balanced for config 3, whose chunks outnumber the
+# resident wave slots; one chunk per wave for config 5's partitions-only
+# kernel).  (3, 0, 20, 1) is the driver's exact timed launch.
+ONE, BAL = abi.SCHED_ONE_PER_WAVE, abi.SCHED_BALANCED
 FULL_SIZE_CASES = [
     (3, 0, 1), (3, 0, 20, 1), (3, 0, 20, 1, ONE), (3, 0, abi.BENCH_STEPS_PER_LAUNCH),
     (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3, ONE),
     (3, 256, 1), (3, 256, abi.BENCH_STEPS_PER_LAUNCH), (3, 256, abi.MAX_STEPS_PER_LAUNCH),
     (5, 0, 1), (5, 0, abi.BENCH_STEPS_PER_LAUNCH), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH),
-    (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (5, 0, 500, 4, ONE),
+    (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (5, 0, 500, 4, ONE), (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 1, BAL),
 ]
 
 
 def _full_id(case):
     c, w, k = case[:3]
     return (f"{c}-{'flat' if w == 0 else f'ring{w}'}-{k}" + (f"-sub{case[3]}" if len(case) > 3 else "")
-            + ("-onewave" if len(case) > 4 and case[4] == ONE else ""))
+            + ("-onewave" if len(case) > 4 and case[4] == ONE else "")
+            + ("-balanced" if len(case) > 4 and case[4] == BAL else ""))
 
 
 @pytest.mark.parametrize("case", FULL_SIZE_CASES, ids=[_full_id(c) for c in FULL_SIZE_CASES])
@@ -492,7 +492,10 @@ def test_full_size_digest(case):
                                    subranges=nsub, schedule=sched, **kw))
     try:
         ce = e.step(meta["steps"])
-        assert e.kernel_info()["balanced"] == (0 if sched == ONE else e.subranges)
+        one = sched == ONE or (sched == abi.SCHED_AUTO and abi.step_net_of(kw) == abi.NET_PART)
+        assert e.kernel_info()["balanced"] == (0 if one else e.subranges)
+        if nsub == 0:
+            assert e.subranges == (3 if abi.step_net_of(kw) == abi.NET_PART else 1)
         if not np.array_equal(ce, want):
             bad = np.argwhere(ce != want)[0]
             raise AssertionError(f"config {cfg}: counters differ at step {bad[0]} ({abi.COUNTER_NAMES[bad[1]]}): "
