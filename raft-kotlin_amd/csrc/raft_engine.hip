@@ -265,8 +265,8 @@ __device__ __forceinline__ Piece piece_of(uint4 pl, int q, int K) {
 // ahead and the youngest starve until they are left alone at low occupancy
 // (measured: waves of equal work ended between 560 and 1,278 us of a 1.28 ms
 // launch, profiles/r4_a3).  Each wave therefore starts at 3 and steps down as
-// its own work runs out (bands of 1/2, 1/4, 3/20 of it, then the last 1/10),
-// so a wave that got ahead yields to the ones behind it.
+// its own work runs out (band_end: at about 1/2, 3/4 and 9/10 of it, earlier
+// for older workgroups), so a wave that got ahead yields to the ones behind it.
 __device__ __forceinline__ void set_priority(int band) {
     if (band >= 3) __builtin_amdgcn_s_setprio(3);
     else if (band == 2) __builtin_amdgcn_s_setprio(2);
@@ -278,13 +278,24 @@ __device__ __forceinline__ uint32_t plan_units(uint4 pl, int K) {
     return pl.x + pl.z * (uint32_t)K + (pl.w != 0 ? (uint32_t)K - pl.w : 0u);
 }
 // chunk-steps from the start of the wave's quarter to the end of band b (b =
-// 3, 2, 1), per mille of its work (tuning builds set other ends)
+// 3, 2, 1): E per mille of its work, shifted by D per mille for each
+// dispatch round of the workgroup from the middle one (slot 0..W-1 of the W
+// workgroups a CU holds; the oldest has slot 0).  The oldest still win every
+// tie on their SIMD, so they step down earlier: slot 0 of 7 at 26 / 63 / 84 %
+// of its work, slot 6 at 74 / 87 / 96 % (-3 to -4 % launch time against
+// unshifted 50 / 75 / 90 %, profiles/r4_o, r4_p).  Tuning builds set others.
 #ifndef RAFT_BAND_ENDS
 #define RAFT_BAND_ENDS 500, 750, 900
 #endif
+#ifndef RAFT_AGE_SHIFTS
+#define RAFT_AGE_SHIFTS 80, 40, 20
+#endif
+template <int W>
 __device__ __forceinline__ uint32_t band_end(uint32_t Q, int b) {
-    constexpr uint32_t E[3] = {RAFT_BAND_ENDS};
-    return (uint32_t)(((uint64_t)Q * E[3 - b]) / 1000u);
+    constexpr int E[3] = {RAFT_BAND_ENDS};
+    constexpr int D[3] = {RAFT_AGE_SHIFTS};
+    const int slot = (int)((blockIdx.x * (uint32_t)W) / gridDim.x);    // wave-uniform
+    return (uint32_t)(((uint64_t)Q * (uint32_t)(E[3 - b] + (2 * slot - (W - 1)) * D[3 - b] / 2)) / 1000u);
 }
 
 // Bounded wait for the previous wave's head piece (never reached by a correct
@@ -330,6 +341,7 @@ template <int R, bool TB, bool RING, int NET>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU(R, TB, RING, NET))))
 void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     using L = Lanes<R>;
+    constexpr int SLOTS = RAFT_STEP_WAVES_PER_EU(R, TB, RING, NET);   // workgroups a CU holds (band_end)
     // LDS: [STEP_WAVES][64][4] the step's Philox job words (Ctx::jl), the
     // tally words, the head-piece flags, then the counter rows [nsteps][NCW]
     extern __shared__ uint32_t lds[];
@@ -376,7 +388,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         const uint32_t Q = plan_units(pl, nsteps);
         // [4]: the band now, [5]: chunk-steps done at its start, [6]: Q
         *(uint4*)(lds_plan + wib * 8 + 4) = make_uint4(3u, 0u, Q, 0u);
-        band_left = bal ? (int)band_end(Q, 3) : 0x7FFFFFFF;
+        band_left = bal ? (int)band_end<SLOTS>(Q, 3) : 0x7FFFFFFF;
         if (bal) set_priority(3);
         const Piece pz = piece_of(pl, 0, nsteps);
         enter_piece<R, RING>(c, n, piece_chunk(pz.chunk));
@@ -431,7 +443,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             const int b = __builtin_amdgcn_readfirstlane((int)bs.x) - 1;
             const uint32_t Q = __builtin_amdgcn_readfirstlane(bs.z);
             set_priority(b);
-            band_left = b > 0 ? (int)(band_end(Q, b) - band_end(Q, b + 1)) : 0x7FFFFFFF;
+            band_left = b > 0 ? (int)(band_end<SLOTS>(Q, b) - band_end<SLOTS>(Q, b + 1)) : 0x7FFFFFFF;
             *(lds_plan + wb * 8 + 4) = (uint32_t)b;
         }
         if (++k == k1) {                           // the piece ends: store its chunk (rare)
