@@ -1169,13 +1169,15 @@ struct Stepper {
             const int32_t t_el = n.elec - P;
             const uint64_t t_fire = t_armed & lm(t_el <= 0);                    // Commons.kt:25-27
             const uint64_t electing = lm(n.fl & FL_ELECTING);                   // T does not change it before use
-            if (!(t_fire | electing)) {
-                n.elec = ib(t_armed) ? t_el : n.elec;
-                send = 0u; sstart = 0; qt = qli = qlt = 0;
-            } else {
+            // the quiet wave's whole update first, so that its path through
+            // the branch is empty (an else-side that redefines the outputs
+            // made the register allocator copy a dozen values on it)
+            n.elec = ib(t_armed) ? t_el : n.elec;
+            send = 0u; sstart = 0; qt = qli = qlt = 0;
+            if (t_fire | electing) {
                 uint32_t f = n.fl;
                 const bool fire = ib(t_fire);
-                n.elec = ib(t_armed) ? (fire ? 0 : t_el) : n.elec;
+                n.elec = fire ? 0 : n.elec;                                     // fire is within t_armed
                 f &= fire ? ~FL_ARMED : ~0u;
                 n.role = fire ? (int32_t)RAFT_CANDIDATE : n.role;               // RaftServer.kt:182
                 cnt.add(t_fire, RAFT_C_TIMEOUTS);
