@@ -1340,6 +1340,9 @@ struct Stepper {
             }
         };
         RAFT_TWICE(PH_V, phase_v(c2, n2, k2, vtodo, lm(vtodo != 0)));
+        // the senders' ballot made here, after H's branch (hoisted above it,
+        // it came back through a VGPR: v_cndmask + v_cmp)
+        asm volatile("" : "+v"(vtodo));
         phase_v(c, n, cnt, vtodo, lm(vtodo != 0));
 
         c.clk.mark(PH_V);
