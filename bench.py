@@ -22,14 +22,17 @@ line then also carries `weak_scaling`, measured in the same job: every GPU its
 own 10^6 groups, timed the same way, whose rank-0 counter rows must equal the
 strong leg's all-reduced rows (the same global groups).  --scaling weak swaps
 the two (the strong leg is then `config4_strong`).  The only collective is the
-all-reduce of the per-step counter rows over RCCL, once the clock has stopped
-(--allreduce inline: per chunk inside the timed region, in series).
+all-reduce of the per-step counter rows over RCCL: one all-reduce of all the
+timed rows, enqueued on the engine stream after the last launch and inside the
+timed region (SURVEY.md §8(e)'s batching: one collective per region; its own
+time is `timing.allreduce_ms`).  --allreduce inline: one per --reduce-every
+chunk, in series with the launches; --allreduce after: once the clock has
+stopped (a diagnostic: the line then times the kernels without the collective).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
-import hashlib
 import importlib
 import json
 import os
@@ -56,7 +59,6 @@ VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
 GROUP_BYTES = 4 * 3
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
-KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h")
 SCHEDULES = {"auto": abi.SCHED_AUTO, "one": abi.SCHED_ONE_PER_WAVE, "balanced": abi.SCHED_BALANCED}
 
 
@@ -68,11 +70,9 @@ def NET_NAMES(net: int) -> list:
 
 def kernel_source_id() -> str:
     """Short hash of the step kernel's sources: a PMC row describes one kernel
-    build, so bench.py attaches it only to a run of the same sources."""
-    h = hashlib.sha1()
-    for f in KERNEL_SOURCES:
-        h.update(open(os.path.join(ROOT, "raft-kotlin_amd", "csrc", f), "rb").read())
-    return h.hexdigest()[:12]
+    build, so bench.py attaches it only to a run of the same sources (the
+    loaded library carries the same id, raft_build_kernel_source_id)."""
+    return importlib.import_module("raft-kotlin_amd.build").kernel_source_id()
 
 
 def shard(total: int, world: int, rank: int, scaling: str) -> tuple[int, int]:
@@ -283,10 +283,11 @@ def parse_args(argv=None):
                          "while that fits 60%% of HBM, else 256 for configs 2 and 3 (DESIGN.md §4.2)")
     ap.add_argument("--reduce-every", type=int, default=512,
                     help="steps per step_async call and per inline counter all-reduce (rounded to whole launches)")
-    ap.add_argument("--allreduce", choices=["after", "inline"], default="after",
-                    help="N > 1: all-reduce the per-step counter rows once after the timed region (they are "
-                         "observations, not the data path), or per --reduce-every chunk inside it, in series "
-                         "with the launches")
+    ap.add_argument("--allreduce", choices=["end", "inline", "after"], default="end",
+                    help="N > 1: all-reduce the timed region's per-step counter rows once, on the engine stream "
+                         "after the last launch, inside the timed region (end); per --reduce-every chunk, in series "
+                         "with the launches (inline); or once the clock has stopped (after: a diagnostic that "
+                         "leaves the collective off the clock)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-general-leg", action="store_true",
                     help="N = 1: skip the general_kernel leg (the main leg on the run-time-decided kernel)")
@@ -382,11 +383,16 @@ def handler_requests(rng, n, G, R, max_term):
     return group, dst, vote, app
 
 
-# the handler batches' algorithmic bytes per message: the
-# message in (group 8 + replica 4 + request), the response out, the replica's
-# 10 scalar fields read and written, and the two log slots its tail cache is
-# derived from; an append also reads log[prev] and writes its entry
-HANDLER_ALG_BYTES = {"vote": 12 + 16 + 8 + 2 * 40 + 16, "append": 12 + 32 + 12 + 2 * 40 + 16 + 8 + 8}
+# the handler batches' algorithmic bytes per message: what
+# the reference's handler itself reads and writes.  The message in (group 8 +
+# replica 4 + request 16 / 32) and the response out (8 / 12).  vote()
+# (RaftServer.kt:228-251) reads 6 fields (term, votedFor, state, lastIndex,
+# physLen, the consumer flags) and log[lastIndex-1].term, and writes at most 5
+# (term, votedFor, state, flags, the re-armed timer).  append() (:253-287)
+# reads 7 (those plus commitIndex) and log[prev].term, writes at most 8 (plus
+# commitIndex, lastIndex, physLen) and one entry.
+HANDLER_ALG_BYTES = {"vote": 12 + 16 + 8 + 4 * 6 + 4 * 5 + 4,
+                     "append": 12 + 32 + 12 + 4 * 7 + 4 * 8 + 4 + 8}
 HANDLER_PMC_FILE = os.path.join(ROOT, "profiles", "pmc_handler.json")
 
 
@@ -517,14 +523,14 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
                                   "pmc_source": pmc["source"] if pmc else None},
                      "parity_messages": msgs, "parity_span_groups": min(G, args.handler_span),
                      "parity_mismatches": int(bad)}
-    out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a key kernel, a stable hipcub radix sort "
-                   "over the key bits, the handler kernel (one lane per replica run, messages in batch order) and "
+    out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a key kernel, a stable rocprim onesweep "
+                   "radix sort over the key bits, the handler kernel (one lane per replica run, messages in batch order) and "
                    "one status synchronisation; _host_buffers: the same through the host entry points from pageable "
                    "arrays (multi-threaded copy into engine-owned pinned staging, PCIe both ways); _pinned_host: from "
                    "page-locked arrays, which the DMA reads and writes directly. The engine holds the bench run's "
                    "final state; the messages are random (bench.handler_requests). roofline: the algorithmic bytes "
-                   "per message (message in, response out, the replica's fields read and written, its tail-cache "
-                   "slots; an append's log[prev] read and entry write) at the device rate; traffic: rocprofv3 "
+                   "per message (HANDLER_ALG_BYTES: message in, response out, the fields the reference's handler reads "
+                   "and writes, its log[lastIndex-1] / log[prev] term read and an append's entry write) at the device rate; traffic: rocprofv3 "
                    "FETCH_SIZE + WRITE_SIZE of every kernel of the batch per message. Parity: a separate batch of "
                    "parity_messages messages over a span of groups, replayed by the oracle's handlers")
     return out
@@ -533,31 +539,36 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
 def timed_leg(eng, args, chunk, coll, dev, world):
     """Warmup (untimed), then the timed region of `args.steps` lockstep steps on
     `eng`: enqueued in chunks of `chunk` steps, bracketed by a barrier and a
-    device sync on both sides; when `coll`, the counter rows all-reduced over
-    the ranks after the clock stops (--allreduce after) or per chunk in series
-    with the launches (inline).  Returns this rank's clock, the stream-event and
-    step-kernel times, the job's elapsed time (MAX over ranks) and the counter
-    rows (this rank's, all ranks', warmup)."""
+    device sync on both sides.  When `coll`, the counter rows are all-reduced
+    over the ranks: by default (--allreduce end) once, on the engine stream
+    after the last launch and before the closing sync, so the collective is
+    inside the clock; per chunk in series with the launches (inline); or after
+    the clock stops (after, a diagnostic).  Returns this rank's clock, the
+    stream-event, step-kernel and all-reduce times, the job's elapsed time (MAX
+    over ranks) and the counter rows (this rank's, all ranks', warmup)."""
     import torch
     import torch.distributed as dist
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
     counters = torch.zeros((args.steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
     gcounters = torch.zeros_like(counters) if coll else counters
     wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+    mode = args.allreduce if coll else None
 
     # ---- warmup (untimed) ----
     comm_stream = torch.cuda.Stream(device=dev)
     if args.warmup:
         eng.step_async(args.warmup, wcount.data_ptr())
     if coll:
-        # the counter all-reduce's first use on its stream (communicator
-        # and stream setup) belongs to the warmup: the warmup rows, all-reduced
-        # exactly as the timed chunks are, twice
-        wev = torch.cuda.Event()
-        wev.record(stream)
-        comm_stream.wait_event(wev)
+        # the counter all-reduce's first use (communicator and stream setup)
+        # belongs to the warmup: the warmup rows all-reduced twice, on the
+        # stream the timed region will use
         wglob = torch.zeros_like(wcount)
-        with torch.cuda.stream(comm_stream):
+        wst = stream if mode == "end" else comm_stream
+        if mode != "end":
+            wev = torch.cuda.Event()
+            wev.record(stream)
+            comm_stream.wait_event(wev)
+        with torch.cuda.stream(wst):
             for _ in range(2):
                 wglob.copy_(wcount)
                 dist.all_reduce(wglob)
@@ -570,12 +581,14 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     eng.set_kernel_timing(True)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    ar0 = torch.cuda.Event(enable_timing=True)
+    ar1 = torch.cuda.Event(enable_timing=True)
     # the chunks' counter rows and events, made before the clock starts (torch
     # tensor indexing in the loop put ~80 us of host time ahead of the first
     # launch, 6 % of the driver's 20-step run)
     plan = [(q, min(chunk, args.steps - q)) for q in range(0, args.steps, chunk)]
     rows = [counters[q].data_ptr() for q, _ in plan]
-    inline = coll and args.allreduce == "inline"
+    inline = mode == "inline"
     chunk_ev = [torch.cuda.Event() for _ in plan] if inline else []
     torch.cuda.synchronize(dev)
     if coll:
@@ -598,19 +611,31 @@ def timed_leg(eng, args, chunk, coll, dev, world):
                 dist.all_reduce(gcounters[done:done + k])
             if done + k < args.steps:
                 eng.wait_stream(comm_stream.cuda_stream)
+    if mode == "end":
+        # the default: every timed row all-reduced once, in series on the
+        # engine stream after the last launch's counter reduction (nothing
+        # runs beside the RCCL kernel), before the closing sync.  The copy
+        # keeps this rank's own rows for its roofline.
+        ar0.record(stream)
+        with torch.cuda.stream(stream):
+            gcounters.copy_(counters)
+            dist.all_reduce(gcounters)
+        ar1.record(stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
     wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
     if coll:
         dist.barrier()
-        if not inline:
-            # the counter rows of every rank, summed once the clock has
-            # stopped: the only collective, and off the data path (the
-            # groups never exchange anything)
+        if mode == "after":
+            # --allreduce after (a diagnostic): the rows of every rank summed
+            # once the clock has stopped, so the line times the kernels alone
+            t_ar = time.perf_counter()
             gcounters.copy_(counters)
             dist.all_reduce(gcounters)
             torch.cuda.synchronize(dev)
+            after_ms = (time.perf_counter() - t_ar) * 1e3
     ev_ms = ev0.elapsed_time(ev1)
+    allreduce_ms = ar0.elapsed_time(ar1) if mode == "end" else (after_ms if mode == "after" else None)
     kern_ms, launches = eng.kernel_time()
     eng.set_kernel_timing(False)
 
@@ -627,7 +652,7 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     else:
         kern_avg_per_rank = [kern_avg_ms]
     return {"wall": wall, "ev_ms": ev_ms, "kern_ms": kern_ms, "launches": launches, "elapsed": elapsed,
-            "kern_avg_ms": kern_avg_ms, "kern_avg_per_rank": kern_avg_per_rank,
+            "kern_avg_ms": kern_avg_ms, "kern_avg_per_rank": kern_avg_per_rank, "allreduce_ms": allreduce_ms,
             "counters": counters, "gcounters": gcounters, "wcount": wcount}
 
 
@@ -669,7 +694,7 @@ def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, s
                                 < abi.MAX_STEPS_PER_LAUNCH),
            "kernel_avg_ms_per_rank": leg["kern_avg_per_rank"],
            "timing": {"wall_ms": leg["wall"] * 1e3, "stream_event_ms": leg["ev_ms"],
-                      "step_kernel_ms_total": leg["kern_ms"]},
+                      "step_kernel_ms_total": leg["kern_ms"], "allreduce_ms": leg["allreduce_ms"]},
            "valid": bad == 0}
     if scaling == "weak":
         out["note"] = ("weak scaling in the same job: every GPU its own --groups groups (contiguous global-id "
@@ -814,7 +839,10 @@ def main(argv=None, result=None):
     kinfo = eng.kernel_info()                                # the timed leg's last launch
     kernel_variant = {"net": kinfo["net"], "net_bits": NET_NAMES(kinfo["net"]), "textbook": bool(kinfo["textbook"]),
                       "ring": bool(kinfo["ring"]), "schedule": "balanced" if kinfo["balanced"] else "one_per_wave",
-                      "workgroups": kinfo["workgroups"], "resident_workgroups": kinfo["resident_workgroups"]}
+                      "workgroups": kinfo["workgroups"], "resident_workgroups": kinfo["resident_workgroups"],
+                      # the loaded library's own provenance (build.py ids compiled in)
+                      "kernel_source_id": abi.build_ids()["kernel_source_id"],
+                      "library_source_id": abi.build_ids()["library_source_id"]}
     c_all = gcounters.cpu().numpy()[:, : abi.NUM_COUNTERS]    # all ranks' groups
     c_loc = counters.cpu().numpy()[:, : abi.NUM_COUNTERS]     # this rank's groups (before the all-reduce)
     value = total_groups * args.steps / elapsed
@@ -968,7 +996,8 @@ def main(argv=None, result=None):
             "subranges": nsub,
             "step_waves_per_rank": -(-G_local // (64 // R)),
             "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window, net) < abi.MAX_STEPS_PER_LAUNCH),
-            "counter_allreduce_every": (chunk if args.allreduce == "inline" else "after_timed_region") if coll else None,
+            "counter_allreduce_every": ({"end": "timed_region_once", "inline": chunk,
+                                         "after": "after_timed_region_diagnostic"}[args.allreduce] if coll else None),
             "collective": ({"backend": backend, "ranks": world, "forced_at_one_rank": world == 1} if coll else None),
         },
         "roofline": {
@@ -995,12 +1024,17 @@ def main(argv=None, result=None):
         "general_kernel": general,
         "roofline_streaming": streaming,
         "timing": {"wall_ms": wall * 1e3, "stream_event_ms": ev_ms, "step_kernel_ms_total": kern_ms,
+                   "allreduce_ms": leg["allreduce_ms"],
                    "note": "the timed region: each rank's wall clock from after the opening barrier + device "
                            "sync to after its closing device sync (the closing barrier follows the clock; the job's "
                            "time is the MAX over ranks), ms_per_step uses the larger of wall and the stream events "
                            "around the launches; step_kernel_ms_total is the time during which a step kernel ran "
                            "(the union of the sub-range launches); the rest is launch latency, the counter "
-                           "reductions, the counter all-reduce (N > 1) and the final sync"},
+                           "reductions, the counter all-reduce and the final sync. allreduce_ms: the all-reduce of "
+                           "the timed counter rows (with its row copy), stream events around it on the engine "
+                           "stream; inside the clock unless counter_allreduce_every says after_timed_region_"
+                           "diagnostic (then host time after the clock stopped); null at one rank without a "
+                           "collective"},
         "valid": overflow == 0 and wmiss == 0 and bad_untimed == 0,
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},

@@ -145,10 +145,11 @@ typedef struct raft_params {
  * A chunk is one wave's 64 / R groups.  ONE_PER_WAVE launches a wave per
  * chunk for all steps of the launch: when the chunks outnumber the GPU's
  * resident wave slots, the last round of waves runs on a part-empty chip.
- * BALANCED launches only the workgroups the GPU holds at once; each takes a
- * contiguous run of chunks and its waves split the run's chunk-steps into
- * equal parts (a chunk may pass from one wave to the next between steps),
- * so every wave ends together.  AUTO takes BALANCED when the chunks
+ * BALANCED launches only the workgroups the GPU holds at once (nb of them);
+ * workgroup b takes the interleaved chunks b, b + nb, b + 2 nb, ... (so the
+ * chunks running at one time are neighbours) and its waves split those
+ * chunks' chunk-steps into equal parts (a chunk may pass from one wave to
+ * the next between steps), so every wave ends together.  AUTO takes BALANCED when the chunks
  * outnumber the resident wave slots, else ONE_PER_WAVE. */
 #define RAFT_SCHED_AUTO         0
 #define RAFT_SCHED_ONE_PER_WAVE 1
@@ -257,6 +258,14 @@ typedef struct raft_engine raft_engine;
 void        raft_params_default(raft_params* p);
 const char* raft_last_error(void);
 int         raft_abi_version(void);
+/* The build's provenance: a short hash of every source, header and compiler
+ * flag the library was built from (raft-kotlin_amd/build.py
+ * library_source_id; abi.load_library refuses a library whose id differs
+ * from the sources beside it), and of the step kernel's three sources
+ * (kernel_source_id, the key of bench.py's rocprofv3 rows).  "unknown" for a
+ * build made without build.py. */
+const char* raft_build_source_id(void);
+const char* raft_build_kernel_source_id(void);
 int raft_engine_create(const raft_params* p, int device, raft_engine** out);
 int raft_engine_destroy(raft_engine* e);
 

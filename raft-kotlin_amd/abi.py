@@ -214,6 +214,29 @@ def _missing_entry(name: str):
     return stub
 
 
+def check_build(lib, p: str) -> None:
+    """Refuse an engine library that was not built from the sources beside it
+    (build.py compiles library_source_id() into it): a stale binary would make
+    every measurement and parity result describe other code.  Skipped when
+    the sources are absent (an installed library)."""
+    from . import build as B
+    if not B.sources_present():
+        return
+    lib.raft_build_source_id.restype = C.c_char_p
+    have = lib.raft_build_source_id().decode()
+    want = B.library_source_id()
+    if have != want:
+        raise RuntimeError(f"{p} was built from sources {have}, the working tree is {want}: rebuild it "
+                           "(`python raft-kotlin_amd/build.py`)")
+
+
+def build_ids() -> dict:
+    """The loaded library's provenance (include/raft_engine.h raft_build_*)."""
+    lib = load_library()
+    return {"library_source_id": lib.raft_build_source_id().decode(),
+            "kernel_source_id": lib.raft_build_kernel_source_id().decode(), "path": LIB_PATH}
+
+
 def load_library(path: str | None = None):
     """Load the HIP engine.  Raises if it is absent: there is no fallback."""
     global _lib
@@ -225,12 +248,16 @@ def load_library(path: str | None = None):
             f"HIP engine library not built: {p} (run `python __graft_entry__.py build` "
             "or `python raft-kotlin_amd/build.py`)")
     lib = C.CDLL(p)
+    if path is None and not os.environ.get("RAFT_ENGINE_LIB"):
+        check_build(lib, p)
     P, I32, I64, U64 = C.POINTER, C.c_int32, C.c_int64, C.c_uint64
     eng = C.c_void_p
     sig = {
         "raft_params_default": (None, [P(raft_params)]),
         "raft_last_error": (C.c_char_p, []),
         "raft_abi_version": (C.c_int, []),
+        "raft_build_source_id": (C.c_char_p, []),
+        "raft_build_kernel_source_id": (C.c_char_p, []),
         "raft_engine_create": (C.c_int, [P(raft_params), C.c_int, P(eng)]),
         "raft_engine_destroy": (C.c_int, [eng]),
         "raft_engine_step": (C.c_int, [eng, I32, P(I64)]),
@@ -294,7 +321,8 @@ def load_library(path: str | None = None):
 
 # symbols declared in include/*.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
-    "raft_params_default", "raft_last_error", "raft_abi_version", "raft_engine_create",
+    "raft_params_default", "raft_last_error", "raft_abi_version", "raft_build_source_id",
+    "raft_build_kernel_source_id", "raft_engine_create",
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",

@@ -204,8 +204,9 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
 //    runs on a part-empty chip (1.25e5 groups: 10,417 waves = 1.45 rounds of
 //    the 7,168 slots).
 //  * Balanced (bal_chunks > 0): the grid is the workgroups the chip holds at
-//    once; workgroup b takes the chunks [b * n / nb, (b + 1) * n / nb) (n =
-//    bal_chunks, nb = gridDim.x, at least STEP_WAVES of them) and its waves
+//    once; workgroup b takes the interleaved chunks b, b + nb, b + 2 nb, ...
+//    (n = bal_chunks, nb = gridDim.x; m = n / nb or one more, at least
+//    STEP_WAVES of them; piece_chunk) and its waves
 //    split the m chunks' m * K chunk-steps into equal quarters (McNaughton's
 //    wrap-around rule).  A quarter [u0, u1) is a head piece (the first e steps
 //    of the chunk it ends in), whole chunks, and a tail piece (the last K - s
@@ -234,8 +235,8 @@ __device__ __forceinline__ uint4 plan_of(int wib, int K) {
     // workgroup b: its i-th chunk is wave0 + b + i * nb (piece_chunk), i < m,
     // m = q or q + 1 (q = n / nb, the first n % nb workgroups take one more):
     // the chunks running at one time are neighbours, as in the one-chunk-per-
-    // wave schedule; the plan holds indices i; 32-bit throughout (the host
-    // keeps m * K < 2^31)
+    // wave schedule; the plan holds indices i; 32-bit throughout (launch_geo
+    // refuses a launch with STEP_WAVES * m * K >= 2^32)
     const uint32_t b = blockIdx.x, q = (uint32_t)kp->bal_q, rem = (uint32_t)kp->bal_rem, k = (uint32_t)K;
     const uint32_t U = (q + (b < rem ? 1u : 0u)) * k;
     const uint32_t u0 = (uint32_t)wib * U / STEP_WAVES, u1 = (uint32_t)(wib + 1) * U / STEP_WAVES;
@@ -300,13 +301,25 @@ __device__ __forceinline__ uint32_t band_end(uint32_t Q, int b) {
 
 // Bounded wait for the previous wave's head piece (never reached by a correct
 // schedule without the flag set; the bound keeps a broken one from hanging the
-// GPU -- its results would then differ from the oracle's).  The flag is set
-// after the producer's stores completed (vmcnt(0)); the producer is on this CU,
-// whose vector L1 is invalidated here before the chunk's state is read.
+// GPU).  A wave that gives up sets RAFT_DEV_WAIT_TIMEOUT in the engine's
+// status word (page-locked host memory, a vector atomic), and the engine's
+// next sync, step or kernel_time returns RAFT_EDEVICE: the launch's results
+// are not the reference's.  The flag is set after the producer's stores
+// completed (vmcnt(0)); the producer is on this CU, whose vector L1 is
+// invalidated here before the chunk's state is read.
 __device__ __forceinline__ void wait_head(const uint32_t* flag) {
+    bool set = false;
     for (uint32_t spins = 0; spins < (1u << 24); ++spins) {
-        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) break;
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) {
+            set = true;
+            break;
+        }
         __builtin_amdgcn_s_sleep(2);
+    }
+    if (!set) {
+        const KernArgs kp = kernargs();
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_or(kp->status, RAFT_DEV_WAIT_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     asm volatile("buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
@@ -1080,6 +1093,11 @@ static int launch_geo(raft_engine* e, StepKernel kern, int k, LaunchGeo& geo) {
         geo.w0[q + 1] = b;
         geo.bal[q] = bal ? n : 0;
         geo.nb[q] = bal ? std::min(cap, n / STEP_WAVES) : e->sub_b0[q + 1] - e->sub_b0[q];
+        // plan_of's 32-bit arithmetic: (wave + 1) * m * K < 2^32 for a
+        // workgroup's m = ceil(n / nb) chunks
+        if (bal && (uint64_t)STEP_WAVES * (uint64_t)((n + geo.nb[q] - 1) / geo.nb[q]) * (uint64_t)k >= (1ull << 32))
+            return fail(RAFT_EINVAL, "balanced launch too long for its workgroups (4 * chunks per workgroup * "
+                                     "steps_per_launch >= 2^32): raise schedule_workgroups or lower steps_per_launch");
         geo.col0[q] = geo.stride;
         geo.stride += geo.nb[q];
         geo.balanced += bal;
@@ -1157,6 +1175,14 @@ void raft_params_default(raft_params* p) {
 
 const char* raft_last_error(void) { return g_err.c_str(); }
 int raft_abi_version(void) { return RAFT_ABI_VERSION; }
+#ifndef RAFT_BUILD_SOURCE_ID
+#define RAFT_BUILD_SOURCE_ID "unknown"
+#endif
+#ifndef RAFT_BUILD_KERNEL_ID
+#define RAFT_BUILD_KERNEL_ID "unknown"
+#endif
+const char* raft_build_source_id(void) { return RAFT_BUILD_SOURCE_ID; }
+const char* raft_build_kernel_source_id(void) { return RAFT_BUILD_KERNEL_ID; }
 
 void raft_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     const u32x4 v = philox4x32_10(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
@@ -1281,6 +1307,12 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.log = (uint2*)b;
     *out = e;
     err = hipHostMalloc((void**)&e->bflags_host, 64, hipHostMallocDefault);
+    if (err == hipSuccess) {
+        // word 8: the step kernel's status word (RAFT_DEV_*), written by the
+        // device and read by the host after a synchronisation
+        e->bflags_host[8] = 0u;
+        err = hipHostGetDevicePointer((void**)&d.status, e->bflags_host + 8, 0);
+    }
     if (err != hipSuccess) {
         raft_engine_destroy(e);
         *out = nullptr;
@@ -1445,10 +1477,21 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
     return RAFT_OK;
 }
 
+// The step kernel's status word, read after a synchronisation of the engine
+// stream (every step launch has finished): nonzero means a launch's results
+// are not the reference's.
+static int check_device_status(raft_engine* e) {
+    const uint32_t s = __atomic_load_n(&e->bflags_host[8], __ATOMIC_ACQUIRE);
+    if (s & RAFT_DEV_WAIT_TIMEOUT)
+        return fail(RAFT_EDEVICE, "a balanced-schedule wave timed out waiting for the previous wave's head piece: "
+                                  "the engine's state is not the reference's (raft_engine_reset clears this)");
+    return RAFT_OK;
+}
+
 int raft_engine_sync(raft_engine* e) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return RAFT_OK;
+    return check_device_status(e);
 }
 
 int raft_engine_step(raft_engine* e, int32_t n_steps, int64_t* counters_host) {
@@ -1462,6 +1505,7 @@ int raft_engine_step(raft_engine* e, int32_t n_steps, int64_t* counters_host) {
             HIP_TRY(hipMemcpyAsync(counters_host + (int64_t)done * RAFT_COUNTER_STRIDE, e->counters_dev,
                                    (size_t)k * RAFT_COUNTER_STRIDE * 8, hipMemcpyDeviceToHost, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
+        if (int rc = check_device_status(e)) return rc;
         done += k;
     }
     return RAFT_OK;
@@ -1513,7 +1557,7 @@ int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches)
     *launches = e->timed_launches;
     e->ev_used = 0;
     e->timed_launches = 0;
-    return RAFT_OK;
+    return check_device_status(e);
 }
 int64_t raft_engine_step_index(raft_engine* e) { return e ? (int64_t)e->t : -1; }
 int raft_engine_set_steps_per_launch(raft_engine* e, int32_t k) {
@@ -1558,6 +1602,7 @@ int raft_engine_reset(raft_engine* e) {
     dispatch_R<InitL>(e->p.R, e);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(e->stream));
+    e->bflags_host[8] = 0u;                // the step kernel's status word
     e->t = 0;
     e->cache_valid = true;                 // init zeroes the tail cache with the logs' lastIndex
     e->iso_written = false;

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-5 GPU sessions, one named preset per call:
+#   gpurun -- 'PRESET=a bash scripts/sessions/r5.sh'
+# Every GPU step has its own time limit and a failure ends the script.
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+P=${PRESET:?set PRESET}
+OUT=gpurun_out/r5_$P; mkdir -p "$OUT"
+step() {   # step NAME LIMIT CMD...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/status.txt"
+  [ $rc -eq 0 ] || exit $rc
+}
+Q="--no-cpu-baseline --handler-batch 0 --no-general-leg --stream-steps 0"
+case $P in
+  a)  # the collective inside the clock: forced one-rank RCCL beside the plain line, full size and 1/8 shard
+      for i in 1 2; do
+        step d20_plain_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step d20_rccl_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        step s8_plain_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_rccl_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      done
+      for f in $OUT/*.log; do
+        echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"allreduce_ms": [0-9.enul]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1)"
+      done > $OUT/summary.txt
+      step pytest 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      TAG=r5_a/dist STEPS=512 step dist 900 bash scripts/dist_rehearsal.sh
+      ;;
+  *) echo "unknown preset $P"; exit 2 ;;
+esac
+exit 0

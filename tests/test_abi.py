@@ -133,3 +133,23 @@ def test_host_alloc_arguments(lib):
     assert lib.raft_host_alloc(0) is None
     assert b"positive" in lib.raft_last_error()
     assert lib.raft_host_free(None) == abi.RAFT_OK
+
+
+def test_library_is_built_from_these_sources(lib):
+    """The loaded engine carries the id of the sources and flags it was built
+    from (build.py library_source_id), equal to the working tree's, and the
+    step kernel's id bench.py keys its rocprofv3 rows on."""
+    B = importlib.import_module("raft-kotlin_amd.build")
+    ids = abi.build_ids()
+    assert ids["library_source_id"] == B.library_source_id() == B.built_source_id()
+    assert ids["kernel_source_id"] == B.kernel_source_id()
+    assert not B.needs_build()
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """abi.load_library refuses a library whose compiled-in source id is not
+    the working tree's (a binary that describes other code)."""
+    B = importlib.import_module("raft-kotlin_amd.build")
+    monkeypatch.setattr(B, "library_source_id", lambda: "0" * 12)
+    with pytest.raises(RuntimeError, match="rebuild"):
+        abi.check_build(abi.load_library(), abi.LIB_PATH)

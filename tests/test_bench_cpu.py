@@ -142,3 +142,11 @@ def test_pmc_parse_launches_of_subrange_dispatches():
     assert pmc_parse.expand([["warmup", 5, 3], ["timed", 20, 3], ["streaming", 1, 1], ["timed", 7]]) == \
         [0, 0, 0, 1, 1, 1, 2, 3]
     assert pmc_parse.union_ms([(0, 10), (5, 20), (30, 40), (35, 38)]) == 30 / 1e6
+
+
+def test_counter_allreduce_is_inside_the_timed_region_by_default():
+    """The N > 1 counter all-reduce (the path's one collective, SURVEY.md
+    §8(e)) is enqueued inside the timed region unless a diagnostic asks
+    otherwise."""
+    assert bench.parse_args([]).allreduce == "end"
+    assert bench.parse_args(["--allreduce", "after"]).allreduce == "after"

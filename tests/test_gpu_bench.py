@@ -4,8 +4,10 @@ The driver runs config 4 (10^6 x 5 sharded over 2/4/8 GPUs) with one RCCL
 communicator per node; a one-GPU box can still execute every line of that
 branch at WORLD_SIZE 1 (RAFT_BENCH_FORCE_COLLECTIVE=1): the `nccl` (RCCL)
 process group created with device_id, the all_reduce of the counter rows
-after the timed region (or per chunk on a side stream, in series with the
-launches: --allreduce inline), and the MAX / all-gather reductions of the elapsed and kernel times.  The
+inside the timed region (the default, --allreduce end: once, on the engine
+stream after the last launch; inline: per chunk on a side stream, in series
+with the launches; after: the diagnostic off the clock), and the MAX /
+all-gather reductions of the elapsed and kernel times.  The
 all-reduced rows must equal this rank's own rows and the CPU oracle's
 counters for the same global groups and steps.  bench.main runs in this
 process (no child process once the GPU is initialised).
@@ -27,7 +29,7 @@ bench = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(bench)
 
 
-@pytest.mark.parametrize("backend,mode", [("nccl", "after"), ("nccl", "inline"), ("gloo", "after")])
+@pytest.mark.parametrize("backend,mode", [("nccl", None), ("nccl", "inline"), ("nccl", "after"), ("gloo", None)])
 def test_forced_collective_at_one_rank(backend, mode, monkeypatch):
     monkeypatch.setenv("RAFT_BENCH_FORCE_COLLECTIVE", "1")
     monkeypatch.setenv("RAFT_BENCH_BACKEND", backend)
@@ -35,12 +37,18 @@ def test_forced_collective_at_one_rank(backend, mode, monkeypatch):
         monkeypatch.delenv(k, raising=False)
     G, warm, steps = 24_000, 40, 800          # two 400-step launches: two all-reduce chunks at --reduce-every 400
     res = {}
-    rc = bench.main(["--groups", str(G), "--steps", str(steps), "--warmup", str(warm), "--stream-steps", "0",
-                     "--reduce-every", "400", "--allreduce", mode, "--no-cpu-baseline"], result=res)
+    argv = ["--groups", str(G), "--steps", str(steps), "--warmup", str(warm), "--stream-steps", "0",
+            "--reduce-every", "400", "--no-cpu-baseline"] + (["--allreduce", mode] if mode else [])
+    rc = bench.main(argv, result=res)
     assert rc == 0
     out = res["out"]
     assert out["config"]["collective"] == {"backend": backend, "ranks": 1, "forced_at_one_rank": True}
-    assert out["config"]["counter_allreduce_every"] == (400 if mode == "inline" else "after_timed_region")
+    # the default is the in-clock mode: one all-reduce of the timed rows before the closing sync
+    want = {None: "timed_region_once", "inline": 400, "after": "after_timed_region_diagnostic"}[mode]
+    assert out["config"]["counter_allreduce_every"] == want
+    if mode is None:
+        ar = out["timing"]["allreduce_ms"]
+        assert ar is not None and 0 < ar < out["timing"]["wall_ms"], "the all-reduce runs inside the clock"
     assert out["valid"] and out["value"] > 0
     ca, cl = res["counters_all"], res["counters_local"]
     assert np.array_equal(ca, cl), "a one-rank all-reduce must return this rank's rows"

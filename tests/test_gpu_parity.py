@@ -334,6 +334,48 @@ def test_kernel_info_names_the_launched_kernel():
     e.close()
 
 
+@pytest.mark.parametrize("cfg", [3, 2])
+def test_reset_then_general_kernel_equals_fresh_engine(cfg):
+    """raft_engine_reset (a restarted node, RaftServer.kt:28-70, for every
+    group) leaves the engine exactly as raft_engine_create does: an engine
+    stepped N steps -- on config 2 after write_state stored an isolation
+    word, which switches it to a NET_ISO kernel (step_net) -- then reset and
+    switched to the general kernel (RAFT_KERNEL_GENERAL) steps N again to the
+    counters, state, logs and digest of a fresh engine and of the oracle."""
+    kw = dict(abi.CONFIGS[cfg], G=3000)
+    if cfg == 3:
+        kw["churn_ppm"] = 20_000
+    steps, cap = 120, 128
+    e = RaftEngine(abi.make_params(log_cap=cap, steps_per_launch=40, **kw))
+    e.step(30)
+    if cfg == 2:
+        st = e.read_state()
+        st[5, -2] = (4 << 8) | 1                          # replica 1 of group 5 isolated for 4 steps
+        e.write_state(st)
+        e.step(1)
+        assert e.kernel_info()["net"] == abi.NET_ALL
+    e.step(steps - 31)
+    e.reset()
+    assert e.step_index == 0
+    e.set_kernel(abi.KERNEL_GENERAL)
+    ce = e.step(steps)
+    assert e.kernel_info()["net"] == abi.NET_ALL
+    f = RaftEngine(abi.make_params(log_cap=cap, steps_per_launch=40, **kw))
+    cf = f.step(steps)
+    if cfg == 2:                                          # the fresh engine runs the partitions-only kernel
+        assert f.kernel_info()["net"] == abi.NET_PART
+    o = O.Oracle(abi.make_params(log_cap=cap, **kw))
+    co = o.step(steps, nthreads=NTHREADS)[:, : abi.NUM_COUNTERS]
+    assert np.array_equal(ce, cf) and np.array_equal(ce, co)
+    se = e.read_state()
+    assert_same_state(se, f.read_state(), kw["R"], "reset vs fresh")
+    assert_same_state(se, o.read_state(), kw["R"], "reset vs oracle")
+    assert_same_logs(se, e.read_log(), o.read_log(), kw["R"], "reset vs oracle")
+    assert e.digest() == f.digest() == o.digest()
+    e.close()
+    f.close()
+
+
 def test_shard_invariance():
     """Config 4's contract: sharding by global group id does not change any group."""
     kw = dict(abi.CONFIGS[3])
@@ -606,45 +648,96 @@ def random_states(rng, n, R, cap):
     return w, logs_t, logs_c
 
 
-@pytest.mark.parametrize("mode,G,n", [(abi.MODE_REFERENCE, 64, 3000), (abi.MODE_TEXTBOOK, 64, 3000),
-                                      (abi.MODE_REFERENCE, 4000, 100_000), (abi.MODE_REFERENCE, 1, 4000)])
-def test_handler_batches_vs_oracle(mode, G, n):
+def random_ring_states(rng, n, R, cap, window):
+    """States for a log_window ring whose handler batches stay inside the
+    window: physLen up to cap (the ring wraps), lastIndex at most window / 2
+    below it, so every Log.get / overwrite the requests below make reads a
+    retained slot."""
+    w, logs_t, logs_c = random_states(rng, n, R, cap)
+    for r in range(R):
+        phys = rng.integers(0, cap + 1, size=n)
+        last = np.maximum(0, phys - rng.integers(0, window // 2, size=n))
+        set_fld(w, R, r, "phys", phys)
+        set_fld(w, R, r, "last", last)
+    return w, logs_t, logs_c
+
+
+def handler_messages(rng, n, G, R, cap, w=None, window=0):
+    """n random (group, dst) and vote / append / command requests; on a ring
+    (window > 0) the indices they read stay within window / 4 of the target's
+    lastIndex (see random_ring_states)."""
+    grp = rng.integers(0, G, size=n)
+    dst = rng.integers(0, R, size=n).astype(np.int32)
+    if window:
+        last = np.array([fld(w[g], R, d, "last") for g, d in zip(grp, dst)])
+        phys = np.array([fld(w[g], R, d, "phys") for g, d in zip(grp, dst)])
+        li = np.maximum(0, last - rng.integers(0, 4, n))
+        prev = last - 1 - rng.integers(0, window // 4, n)
+        prev = np.where(prev < phys - window + window // 4, np.maximum(last - 1, -1), prev)
+        prev = np.where((prev < 0) & (phys > window // 2), last - 1, np.maximum(prev, -1))
+    else:
+        li = rng.integers(0, cap + 1, n)
+        prev = rng.integers(-1, cap, n)
+    vq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), li, rng.integers(0, 4, n)],
+                  axis=1).astype(np.int32)
+    aq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), prev,
+                   rng.integers(-1, 4, n), rng.integers(0, 2, n), rng.integers(0, 6, n),
+                   rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)], axis=1).astype(np.int64)
+    cmd = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    return grp, dst, vq, aq, cmd
+
+
+HANDLER_CASES = [
+    # (R, mode, G, n, log_window): long per-replica runs (G = 64 groups: ~15-50
+    # messages per replica), many replicas (10^5 messages), one group (runs of
+    # ~800 per replica through the radix sort's passes), and the ring
+    *[(R, abi.MODE_REFERENCE, 64, 10_000, 0) for R in (3, 5, 7)],
+    *[(R, abi.MODE_REFERENCE, 4000, 100_000, 0) for R in (3, 5, 7)],
+    (5, abi.MODE_TEXTBOOK, 64, 3000, 0), (7, abi.MODE_TEXTBOOK, 64, 3000, 0),
+    (5, abi.MODE_REFERENCE, 1, 4000, 0),
+    *[(R, abi.MODE_REFERENCE, 2000, 10_000, 64) for R in (3, 5, 7)],
+]
+
+
+@pytest.mark.parametrize("R,mode,G,n,window", HANDLER_CASES,
+                         ids=[f"R{c[0]}-{'tb' if c[1] else 'ref'}-G{c[2]}-n{c[3]}-w{c[4]}" for c in HANDLER_CASES])
+def test_handler_batches_vs_oracle(R, mode, G, n, window):
     """The single-handler batches (RaftServer.vote() / append() /
     appendCommand(), RaftServer.kt:228-287, :100-107) against the oracle's
-    handlers message by message: at n = 3000 on 64 groups (long runs of
-    messages per replica), at n = 10^5 on 4000 groups, and 4000 messages to
-    one group (runs of ~800 per replica through the radix sort's passes)."""
-    rng = np.random.default_rng(7)
-    R, cap = 5, 8
-    w, lt, lc = random_states(rng, G, R, cap)
-    e, o = pair(R=R, G=G, log_cap=cap, seed=3, mode=mode)
+    handlers message by message, at the replica counts of every BASELINE
+    configuration (R = 3, 5, 7; batch_kernel takes R at run time), on a flat
+    log and on a 64-slot log_window ring whose rows have wrapped."""
+    rng = np.random.default_rng(7 + R + 10 * window)
+    cap = 160 if window else 8
+    if window:
+        w, lt, lc = random_ring_states(rng, G, R, cap, window)
+    else:
+        w, lt, lc = random_states(rng, G, R, cap)
+    e, o = pair(R=R, G=G, log_cap=cap, log_window=window, seed=3, mode=mode)
     for x in (e, o):
         x.write_state(w)
         x.write_log(lt, lc)
-    grp = rng.integers(0, G, size=n)
-    dst = rng.integers(0, R, size=n).astype(np.int32)
-    vq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(0, cap + 1, n),
-                   rng.integers(0, 4, n)], axis=1).astype(np.int32)
+    grp, dst, vq, aq, cmd = handler_messages(rng, n, G, R, cap, w, window)
     ve = e.vote_batch(grp, dst, vq)
     vo = np.array([o.vote(int(g), int(d), *map(int, q)) for g, d, q in zip(grp, dst, vq)], dtype=np.int32)
-    assert np.array_equal(ve, vo)
-    aq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(-1, cap, n),
-                   rng.integers(-1, 4, n), rng.integers(0, 2, n), rng.integers(0, 6, n),
-                   rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)], axis=1).astype(np.int64)
+    assert np.array_equal(ve, vo), f"vote responses differ at {np.argwhere(np.any(ve != vo, axis=1))[:3].ravel()}"
     ae = e.append_batch(grp, dst, aq)
     ao = []
     for g, d, q in zip(grp, dst, aq):
         t, s, st = o.append(int(g), int(d), int(q[0]), int(q[1]), int(q[2]), int(q[3]),
                             (int(q[5]), int(q[6])) if q[4] else None, int(q[7]))
         ao.append((t, int(s), st))
-    assert np.array_equal(ae, np.array(ao, dtype=np.int32))
-    cmd = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    ao = np.array(ao, dtype=np.int32)
+    assert np.array_equal(ae, ao), f"append responses differ at {np.argwhere(np.any(ae != ao, axis=1))[:3].ravel()}"
     e.append_command_batch(grp, dst, cmd)
     for g, d, c in zip(grp, dst, cmd):
         o.append_command(int(g), int(d), int(c))
     se = e.read_state()
     assert_same_state(se, o.read_state(), R, "handlers")
     assert_same_logs(se, e.read_log(), o.read_log(), R, "handlers")
+    if window:
+        # the rows wrapped: some replica holds more physical slots than the ring
+        assert int(np.max(se[:, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(R)]])) > window
 
 
 def test_pinned_host_batches_match_pageable():
