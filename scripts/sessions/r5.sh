@@ -30,6 +30,16 @@ case $P in
       step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       TAG=r5_a/dist STEPS=512 step dist 900 bash scripts/dist_rehearsal.sh
       ;;
+  b)  # issue costs of the Philox instructions; per-phase VALU / SALU budgets of the driver's launch
+      # and of the default (steady-state) launch
+      step ubench 200 scripts/ubench/valu_rate3
+      TAG=r5_b_d20 step phase_d20 900 bash scripts/phase_budget.sh
+      TAG=r5_b_def ARGS=" " step phase_def 900 bash scripts/phase_budget.sh
+      ;;
+  pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
+      TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
+      TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
