@@ -305,6 +305,10 @@ def parse_args(argv=None):
     ap.add_argument("--plan-file", default="",
                     help="write the step-kernel launch sequence (leg, steps) and the workload key as JSON, for "
                          "attributing rocprofv3 dispatches (scripts/pmc_bench.sh)")
+    ap.add_argument("--traffic-probe", action="store_true",
+                    help="after the timed legs (untimed): raft_engine_traffic_probe dispatches (the step kernel's own "
+                         "state and log-store access patterns over known bytes), recorded in --plan-file for "
+                         "calibrating rocprofv3's FETCH_SIZE / WRITE_SIZE in the same process (scripts/pmc_bench.sh)")
     ap.add_argument("--plan-only", action="store_true",
                     help="no GPU: start the ranks, agree on the shards over gloo, print them (tests)")
     return ap.parse_args(argv)
@@ -927,6 +931,13 @@ def main(argv=None, result=None):
                      "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
                      "kernel_group_steps_per_s": G_local / (s_avg / 1e3)}
 
+    # ---- traffic probes (untimed, --traffic-probe): the step kernel's own
+    # access patterns over known bytes, for the PMC byte factors ----
+    probes = []
+    if args.traffic_probe:
+        for kind in ((0, 1) if window == 0 else (0,)):
+            for _ in range(3):
+                probes.append([kind, *eng.traffic_probe(kind)])
     if args.plan_file and rank == 0:
         # [leg, steps, dispatches]: a launch of the warmup / timed legs is one
         # step-kernel dispatch per sub-range; the streaming leg runs one range
@@ -935,7 +946,11 @@ def main(argv=None, result=None):
             seq += [["general_warmup", x, nsub] for x in launch_plan(args.warmup, L)]
             seq += [["general", x, nsub] for x in timed_plan]
         seq += [["streaming", 1, 1]] * args.stream_steps
-        json.dump({"key": pmc_key, "stream_steps": args.stream_steps, "R": R, "launches": seq},
+        ix = abi.C_INDEX
+        stores = float(c_loc[:, ix["entry_writes"]].sum() + c_loc[:, ix["commands"]].sum()) / max(1, launches)
+        json.dump({"key": pmc_key, "stream_steps": args.stream_steps, "R": R, "launches": seq, "probes": probes,
+                   "state_bytes_per_launch": 2 * G_local * (R * REPLICA_BYTES + GROUP_BYTES),
+                   "log_stores_per_timed_launch": stores},
                   open(args.plan_file, "w"))
 
     # ---- safety flags (untimed): the run's counter-borne flags plus the
@@ -1010,6 +1025,15 @@ def main(argv=None, result=None):
             "alg_bytes_per_launch": bytes_alg / max(1, launches),
             "alg_bytes_per_group_step": bytes_alg / max(1, G_local * c_loc.shape[0]),
             "pmc_source": pmc["source"] if pmc else None,
+            # the PMC counts behind `traffic`: raw FETCH_SIZE / WRITE_SIZE
+            # kilobytes per launch and the byte factors of the same process's
+            # traffic probes (scripts/pmc_parse.py probe_factors)
+            "traffic_raw_kb": ({"fetch": pmc.get("fetch_kb_raw"), "write": pmc.get("write_kb_raw")} if pmc else None),
+            "traffic_split": ({"fetch_bytes": pmc.get("fetch_bytes_per_launch"),
+                               "write_bytes": pmc.get("write_bytes_per_launch"),
+                               "log_stores": pmc.get("log_stores_per_launch"),
+                               "fetch_factor": pmc.get("fetch_factor"), "write_factor": pmc.get("write_factor"),
+                               "probes": pmc.get("traffic_probes")} if pmc else None),
             "state_bytes_per_launch": bytes_state / max(1, launches),
             "achieved_state_crossing": achieved_state,
             "frac_state_crossing": achieved_state / HBM_PEAK_GBS,

@@ -317,6 +317,14 @@ int     raft_engine_set_step_index(raft_engine* e, int64_t t);
  * grow-only staging of the handler batches and accessors (kept for the
  * engine's lifetime at 1.25x the largest request; raft_engine_trim_staging
  * frees it, page-locked host staging included). */
+/* Traffic probe (rocprofv3 calibration; never part of a step): kind 0 moves
+ * every chunk's state into registers and back exactly as a step launch's
+ * piece entry and exit does (values unchanged); kind 1 makes one 8-byte store
+ * per replica into its own log row past its last entry (a flat log only), the
+ * Log.add pattern (Commons.kt:56-68).  Returns the bytes the probe's one
+ * dispatch reads and writes, so FETCH_SIZE / WRITE_SIZE of that dispatch
+ * give the counters' byte factors for the step kernel's own access widths. */
+int raft_engine_traffic_probe(raft_engine* e, int32_t kind, int64_t* bytes_read, int64_t* bytes_written);
 int64_t raft_engine_device_bytes(raft_engine* e);
 int     raft_engine_trim_staging(raft_engine* e);
 

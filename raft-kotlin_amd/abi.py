@@ -284,6 +284,7 @@ def load_library(path: str | None = None):
         "raft_engine_digest": (C.c_int, [eng, P(U64)]),
         "raft_engine_digest_range": (C.c_int, [eng, I64, I64, P(U64)]),
         "raft_engine_check_log_matching": (C.c_int, [eng, I64, I64, P(C.c_uint8), P(I64)]),
+        "raft_engine_traffic_probe": (C.c_int, [eng, I32, P(I64), P(I64)]),
         "raft_vote_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_vote_req), P(raft_vote_resp), I64]),
         "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
         "raft_append_command_batch": (C.c_int, [eng, P(I64), P(I32), P(C.c_uint32), I64]),
@@ -330,7 +331,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_set_kernel", "raft_engine_reset", "raft_engine_trim_staging",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
-    "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_vote_batch", "raft_append_batch",
+    "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_engine_traffic_probe", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_vote_batch_dev", "raft_append_batch_dev", "raft_append_command_batch_dev",
     "raft_philox4x32_10", "raft_host_alloc", "raft_host_free",
     # include/raft_wire.h

@@ -513,6 +513,43 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     }
 }
 
+// Traffic probes (rocprofv3 calibration of FETCH_SIZE / WRITE_SIZE; never on
+// the step path): the step kernel's own HBM access patterns over a known
+// byte count, in the same process and on the same box as the launches they
+// calibrate.  One wave per chunk, the step kernel's lane geometry.
+//  kind 0: each chunk's state into VGPRs and back, exactly as a piece's entry
+//          and exit (load_node / store_node): G * (R * 60 + 12) bytes read and
+//          the same written, values unchanged.
+//  kind 1: one 8-byte store per replica into its own log row at slot physLen
+//          (a flat log's slot past the last entry, never read), the pattern of
+//          Log.add (Commons.kt:56-68): 8 bytes per store, counted in *stores.
+template <int R>
+__global__ __launch_bounds__(BLOCK) void traffic_probe_kernel(DevParams p, int kind, int nwaves,
+                                                              unsigned long long* stores) {
+    constexpr int GPW = 64 / R;
+    const int w = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (w >= nwaves) return;                                            // wave-uniform
+    const int lane = threadIdx.x & 63, j = lane / R, r = lane - j * R;
+    const int64_t g = (int64_t)w * GPW + j;
+    const bool live = j < GPW && g < p.G;
+    const int64_t idx = g * R + r;
+    if (kind == 0) {
+        Node n;
+        if (live) load_node(n, p, g, idx);
+        else inert_node(n);
+        asm volatile("" : "+v"(n.term), "+v"(n.voted), "+v"(n.role), "+v"(n.commit), "+v"(n.last), "+v"(n.phys));
+        asm volatile("" : "+v"(n.elec), "+v"(n.fl), "+v"(n.phase), "+v"(n.retry), "+v"(n.t1), "+v"(n.t2), "+v"(n.c1));
+        asm volatile("" : "+v"(n.nx), "+v"(n.mc), "+v"(n.iso), "+v"(n.cmdc), "+v"(n.s0));
+        if (live) store_node(n, p, g, idx, r == 0);
+    } else {
+        const int32_t phys = live ? p.st[fidx(p, RAFT_F_PHYS, idx)] : p.cap;
+        const bool st = phys < p.cap;
+        if (st) p.log[((int64_t)w * 64 + lane) * p.nslots + phys] = make_uint2(0u, 0u);
+        const uint64_t b = __ballot(st);
+        if (lane == 0 && b) atomicAdd(stores, (unsigned long long)__popcll(b));
+    }
+}
+
 // the log of replica idx = g * R + r outside the step kernel: lane
 // (g % GPW) * R + r of the block of step-kernel wave g / GPW
 __device__ __forceinline__ LogView log_of(const DevParams& p, int64_t idx) {
@@ -1241,6 +1278,12 @@ template <int R> struct UnpackL {
         unpack_kernel<R><<<(unsigned)((n + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp, g0, n, buf);
     }
 };
+template <int R> struct ProbeL {
+    static void run(raft_engine* e, int kind, unsigned long long* stores) {
+        const unsigned grid = (unsigned)((e->nwaves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+        traffic_probe_kernel<R><<<grid, BLOCK, 0, e->stream>>>(e->dp, kind, e->nwaves, stores);
+    }
+};
 template <int R> struct LogMatchL {
     static void run(raft_engine* e, int64_t g0, int64_t n, uint8_t* flags, unsigned long long* count) {
         const unsigned grid = (unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
@@ -1910,6 +1953,29 @@ int raft_engine_digest_range(raft_engine* e, int64_t g0, int64_t n, uint64_t* ou
     }
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    return RAFT_OK;
+}
+
+int raft_engine_traffic_probe(raft_engine* e, int32_t kind, int64_t* bytes_read, int64_t* bytes_written) {
+    if (!e || !bytes_read || !bytes_written) return fail(RAFT_EINVAL, "null argument");
+    if (kind != 0 && kind != 1) return fail(RAFT_EINVAL, "kind must be 0 (state) or 1 (log stores)");
+    if (kind == 1 && e->p.log_window) return fail(RAFT_EINVAL, "the log-store probe needs a flat log (log_window 0)");
+    HIP_TRY(hipSetDevice(e->device));
+    e->fork_needed = true;
+    if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, 8)) return rc;
+    unsigned long long* d = (unsigned long long*)e->aux;
+    unsigned long long h = 0;
+    hipError_t err = hipMemsetAsync(d, 0, 8, e->stream);
+    if (err == hipSuccess) {
+        dispatch_R<ProbeL>(e->p.R, e, (int)kind, d);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) err = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
+    const int64_t state = e->p.G * ((int64_t)e->p.R * (4 * F_DEV + 8) + 4 * GX_WORDS);
+    *bytes_read = kind == 0 ? state : 4 * e->p.G * e->p.R;               // kind 1 reads physLen
+    *bytes_written = kind == 0 ? state : 8 * (int64_t)h;
     return RAFT_OK;
 }
 

@@ -196,6 +196,15 @@ class RaftEngine:
                                                              C.byref(out)), "check_log_matching")
         return (int(out.value), f) if flags else int(out.value)
 
+    def traffic_probe(self, kind: int) -> tuple[int, int]:
+        """raft_engine_traffic_probe: one dispatch of the step kernel's own HBM
+        access pattern (kind 0: the state into registers and back; kind 1: one
+        8-byte log store per replica, flat logs only); returns (bytes read,
+        bytes written) for calibrating rocprofv3's FETCH_SIZE / WRITE_SIZE."""
+        r, w = C.c_int64(), C.c_int64()
+        self._check(self._lib.raft_engine_traffic_probe(self._h, int(kind), C.byref(r), C.byref(w)), "traffic_probe")
+        return int(r.value), int(w.value)
+
     # -- the service boundary (RaftServer.kt:228-287, :100-107) -------------
     @staticmethod
     def _batch_index(group, dst, n: int, what: str):

@@ -4,8 +4,9 @@
 #   1. a --kernel-trace --stats run (per-kernel average durations);
 #   2. PMC passes, one counter group per run and never combined with tracing:
 #      FETCH_SIZE | WRITE_SIZE | SQ instruction counts + GRBM_GUI_ACTIVE;
-#   3. the calibration engine (scripts/traffic_run.py calib) under FETCH_SIZE
-#      and WRITE_SIZE, whose launches move a known byte count;
+#   3. the same passes count bench.py's traffic probes (--traffic-probe:
+#      raft_engine_traffic_probe dispatches of the step kernel's own state
+#      and log-store access patterns over known bytes, in the same process);
 #   4. scripts/pmc_parse.py: per-launch rows keyed by the workload and launch
 #      length in $OUT/rows.json; back here, `python scripts/pmc_parse.py
 #      --merge gpurun_out/pmc_*/rows.json` folds them into
@@ -16,7 +17,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_${TAG:-x}
 mkdir -p "$OUT"
-A="${ARGS:-} --no-cpu-baseline --plan-file $OUT/plan.json"
+A="${ARGS:-} --no-cpu-baseline --traffic-probe --plan-file $OUT/plan.json"
 echo "trace" >> "$OUT/status.txt"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python bench.py $A > "$OUT/trace.log" 2>&1 || exit $?

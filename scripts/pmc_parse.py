@@ -6,10 +6,15 @@ workload key and launch length).
 Every step_kernel dispatch of a PMC pass is matched, in dispatch order, to
 the launch sequence bench.py wrote (--plan-file: warmup, timed and streaming
 launches with their step counts).  FETCH_SIZE / WRITE_SIZE are kilobytes per
-dispatch; the calibration engine, whose launches move exactly
-G * (R * 60 + 12) bytes, converts them to bytes for this kernel's 4-byte
-per-lane access pattern (MI355X_MICROARCH.md calibrates gfx950's factor for
-16 B/lane streams only)."""
+dispatch.  The byte factors come from the traffic probes of the same bench
+process (bench.py --traffic-probe, raft_engine_traffic_probe): kind 0 moves
+exactly the state a launch moves, with the step kernel's own 4-byte-per-lane
+loads and stores; kind 1 makes one 8-byte log store per replica into its own
+row, the Log.add pattern.  MI355X_MICROARCH.md calibrates gfx950's factor
+for 16 B/lane streams only, and a separate calibration process's factor
+varied 1.30-1.86 between boxes (round 4).  The step kernel's writes are
+split by the plan's log-store count: the state part at the state factor, each
+log store at the 32-B sector gfx950 writes for it (profiles/r3_l)."""
 import csv
 import glob
 import json
@@ -19,19 +24,17 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
-CALIB_G, CALIB_R = int(os.environ.get("TRAFFIC_GROUPS", "1000000")), 5
-REPLICA_BYTES, GROUP_BYTES = 4 * 13 + 8, 12
 ID_FIELDS = ("config", "mode", "groups", "warmup", "steps", "log_window", "leg", "launch_steps", "stream_steps",
              "kernel_src", "ae_max_entries")
 
 
-def dispatches(d):
-    """{counter: [value per step_kernel dispatch, in dispatch order]}; rows of
+def dispatches(d, kernel="step_kernel"):
+    """{counter: [value per `kernel` dispatch, in dispatch order]}; rows of
     one dispatch (per-XCD or per-SE instances) are summed."""
     acc = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if "step_kernel" in row["Kernel_Name"]:
+            if kernel in row["Kernel_Name"]:
                 acc[row["Counter_Name"]][int(row["Dispatch_Id"])] += float(row["Counter_Value"])
     return {c: [v for _, v in sorted(x.items())] for c, x in acc.items()}
 
@@ -73,14 +76,39 @@ def mean(xs):
     return sum(xs) / len(xs) if xs else None
 
 
+SECTOR = 32          # bytes gfx950 writes for one lane's 8-byte store (profiles/r3_l)
+
+
+def probe_factors(d, plan):
+    """(fetch factor, state write factor, details) from the traffic probes'
+    dispatches in the FETCH_SIZE / WRITE_SIZE passes (bench.py --traffic-probe:
+    3 dispatches of kind 0, then 3 of kind 1 on a flat log)."""
+    probes = plan.get("probes") or []
+    f = {c: v for p in glob.glob(f"{d}/pmc*") for c, v in dispatches(p, "traffic_probe_kernel").items()
+         if c in ("FETCH_SIZE", "WRITE_SIZE")}
+    if not probes or len(f.get("FETCH_SIZE", [])) != len(probes) or len(f.get("WRITE_SIZE", [])) != len(probes):
+        raise SystemExit(f"{d}: the traffic probes are missing (bench.py --traffic-probe)")
+    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+    k0 = [i for i, p in enumerate(probes) if p[0] == 0]
+    k1 = [i for i, p in enumerate(probes) if p[0] == 1]
+    ff = med([probes[i][1] / (f["FETCH_SIZE"][i] * 1024.0) for i in k0])
+    wf = med([probes[i][2] / (f["WRITE_SIZE"][i] * 1024.0) for i in k0])
+    out = {"state_fetch_factor": ff, "state_write_factor": wf,
+           "state_probe_fetch_kb_raw": [f["FETCH_SIZE"][i] for i in k0],
+           "state_probe_write_kb_raw": [f["WRITE_SIZE"][i] for i in k0],
+           "state_probe_bytes_each_way": probes[k0[0]][1]}
+    if k1:
+        stores = probes[k1[0]][2] / 8.0
+        out.update({"log_store_probe_stores": stores,
+                    "log_store_raw_bytes_per_store": med([f["WRITE_SIZE"][i] * 1024.0 / stores for i in k1]),
+                    "log_store_probe_write_kb_raw": [f["WRITE_SIZE"][i] for i in k1]})
+    return ff, wf, out
+
+
 def main(d):
     plan = json.load(open(os.path.join(d, "plan.json")))
     seq = plan["launches"]
-    state = CALIB_G * (CALIB_R * REPLICA_BYTES + GROUP_BYTES)
-    cf = sorted(dispatches(f"{d}/calib_FETCH_SIZE").get("FETCH_SIZE", []))
-    cw = sorted(dispatches(f"{d}/calib_WRITE_SIZE").get("WRITE_SIZE", []))
-    ff = state / (cf[len(cf) // 2] * 1024.0)
-    wf = state / (cw[len(cw) // 2] * 1024.0)
+    ff, wf, probe = probe_factors(d, plan)
     owner = expand(seq)
     per = {}
     for p in sorted(glob.glob(f"{d}/pmc*")):
@@ -107,12 +135,22 @@ def main(d):
         if leg == "streaming":
             key["stream_steps"] = plan["stream_steps"]
         row = dict(key)
+        # writes: the log stores (the plan's count for the timed leg) at the
+        # 32-B sector each costs, the rest (state) at the probe's state factor
+        ls = plan.get("log_stores_per_timed_launch", 0.0) if leg == "timed" else None
+        raw_w = m["WRITE_SIZE"] * 1024.0
+        per_store = probe.get("log_store_raw_bytes_per_store")
+        if ls is not None and per_store:
+            write_b = max(0.0, raw_w - ls * per_store) * wf + ls * SECTOR
+        else:
+            write_b = raw_w * wf
         row.update({
-            "hbm_bytes_per_launch": m["FETCH_SIZE"] * 1024.0 * ff + m["WRITE_SIZE"] * 1024.0 * wf,
+            "hbm_bytes_per_launch": m["FETCH_SIZE"] * 1024.0 * ff + write_b,
             "fetch_bytes_per_launch": m["FETCH_SIZE"] * 1024.0 * ff,
-            "write_bytes_per_launch": m["WRITE_SIZE"] * 1024.0 * wf,
+            "write_bytes_per_launch": write_b,
             "fetch_kb_raw": m["FETCH_SIZE"], "write_kb_raw": m["WRITE_SIZE"],
-            "fetch_factor": ff, "write_factor": wf, "calib_state_bytes": state,
+            "fetch_factor": ff, "write_factor": wf, "traffic_probes": probe,
+            "log_stores_per_launch": ls, "state_bytes_per_launch": plan.get("state_bytes_per_launch"),
             "valu_per_launch": m.get("SQ_INSTS_VALU"), "salu_per_launch": m.get("SQ_INSTS_SALU"),
             "lds_per_launch": m.get("SQ_INSTS_LDS"), "smem_per_launch": m.get("SQ_INSTS_SMEM"),
             "waves": m.get("SQ_WAVES"), "wave_cycles": m.get("SQ_WAVE_CYCLES"),

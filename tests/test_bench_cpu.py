@@ -150,3 +150,24 @@ def test_counter_allreduce_is_inside_the_timed_region_by_default():
     otherwise."""
     assert bench.parse_args([]).allreduce == "end"
     assert bench.parse_args(["--allreduce", "after"]).allreduce == "after"
+
+
+def test_pmc_parse_probe_factors(tmp_path):
+    """The byte factors come from the traffic probes of the same bench process:
+    the state probe's known bytes over its FETCH_SIZE / WRITE_SIZE kilobytes,
+    and the raw write bytes counted per 8-byte log store."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import pmc_parse
+    state, stores = 312_000_000, 4_000_000
+    probes = [[0, state, state]] * 3 + [[1, 20_000_000, 8 * stores]] * 3
+    for i, (counter, vals) in enumerate((("FETCH_SIZE", [state / 1024 / 1.5] * 3 + [10.0] * 3),
+                                         ("WRITE_SIZE", [state / 1024 / 1.25] * 3 + [stores * 64 / 1024] * 3))):
+        d = tmp_path / f"pmc{i + 1}" / "host"
+        d.mkdir(parents=True)
+        with open(d / "run_counter_collection.csv", "w") as f:
+            f.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
+            for k, v in enumerate(vals):
+                f.write(f"{100 + k},traffic_probe_kernel<5>,{counter},{v}\n")
+    ff, wf, info = pmc_parse.probe_factors(str(tmp_path), {"probes": probes})
+    assert abs(ff - 1.5) < 1e-9 and abs(wf - 1.25) < 1e-9
+    assert info["log_store_probe_stores"] == stores and abs(info["log_store_raw_bytes_per_store"] - 64) < 1e-9
