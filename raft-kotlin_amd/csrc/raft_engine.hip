@@ -11,6 +11,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -887,15 +888,27 @@ struct BatchCounters {
 // Key: uint32_t while G * R < 2^32 - 1, else uint64_t; the largest value is
 // the "no replica" key of a message outside the engine.
 constexpr int RUN_MAX = 64;
+
+// The locality pass of the claim path: a stable radix sort of (key, message
+// index) over the key's top LOCALITY_BITS bits only (one onesweep pass), so
+// that the handler threads of a workgroup touch a narrow range of replicas
+// and share cache lines of the field arrays (batch order within a replica is
+// kept by the claim chains, not by the sort).  Batches below LOCALITY_MIN
+// messages skip it.  RAFT_BATCH_LOCALITY_BITS (environment, read at create;
+// tuning) overrides the width, 0 disables the pass.
+constexpr int LOCALITY_BITS = 8;
+constexpr int LOCALITY_MIN = 1 << 16;
 constexpr int RUN_REG = 4;                     // runs this short sort in registers
 
 template <class Key>
 __global__ __launch_bounds__(BLOCK) void batch_claim_kernel(const int64_t* __restrict__ group,
                                                             const int32_t* __restrict__ dst, int n, int64_t G, int R,
                                                             Key* __restrict__ keys, uint2* __restrict__ claim,
-                                                            uint32_t* __restrict__ nxt, unsigned int* flags) {
+                                                            uint32_t* __restrict__ nxt, uint32_t* __restrict__ ord,
+                                                            unsigned int* flags) {
     const int m = blockIdx.x * BLOCK + threadIdx.x;
     if (m >= n) return;
+    if (ord) ord[m] = (uint32_t)m;                                      // the locality sort's values
     const int64_t g = group[m];
     const int32_t d = dst[m];
     if (!(g >= 0 && g < G && d >= 0 && d < R)) {
@@ -967,12 +980,18 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
 // path with its count in place.
 template <bool TB, class Key, int kind>
 __global__ __launch_bounds__(BLOCK) void batch_apply_kernel(DevParams p, uint32_t t, int n,
-                                                            const Key* __restrict__ keys, uint2* __restrict__ claim,
+                                                            const Key* __restrict__ keys,
+                                                            const uint32_t* __restrict__ order,
+                                                            uint2* __restrict__ claim,
                                                             const uint32_t* __restrict__ nxt, const void* req,
                                                             void* resp, unsigned int* flags) {
-    const int m = blockIdx.x * BLOCK + threadIdx.x;
-    if (m >= n) return;
-    const Key key = keys[m];
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    // order (nullable): the messages partially sorted by replica, so that
+    // neighbouring threads touch neighbouring replicas' fields; keys[i] is
+    // then the key of message order[i]
+    const int m = order ? (int)order[i] : i;
+    const Key key = keys[i];
     if (key == ~(Key)0) return;                                         // outside the engine
     const uint2 w = claim[key];
     if (w.y != (uint32_t)m) return;                                     // not its run's leader
@@ -1118,6 +1137,7 @@ struct raft_engine {
     size_t bst2_bytes;
     uint2* claim;               // [G * R] {count, head} per replica, zero between batches
     size_t claim_bytes;
+    int locality_bits;          // the claim path's locality sort (LOCALITY_BITS; 0 = none)
     char* bio;
     size_t bio_bytes;
     char* hst;
@@ -1389,6 +1409,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->bst_bytes = e->bst2_bytes = e->bio_bytes = e->hst_bytes = 0;
     e->claim = nullptr;
     e->claim_bytes = 0;
+    e->locality_bits = LOCALITY_BITS;
+    if (const char* lbv = std::getenv("RAFT_BATCH_LOCALITY_BITS")) e->locality_bits = std::max(0, std::atoi(lbv));
     e->bflags_host = nullptr;
     e->aux = nullptr;
     e->aux_bytes = 0;
@@ -2024,26 +2046,49 @@ static int ensure_claim(raft_engine* e) {
     return RAFT_OK;
 }
 
+
 extern "C++" template <class Key>
 static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
                           void* resp, int n) {
     const int R = e->p.R;
     if (int rc = ensure_claim(e)) return rc;
+    int bits = 1;                                 // key bits; the outside-the-engine key ~0 sorts last
+    while (bits < (int)(8 * sizeof(Key)) && (((uint64_t)e->dp.GR - 1) >> bits)) ++bits;
+    const int lb = n >= LOCALITY_MIN ? std::min(e->locality_bits, bits) : 0;
+    size_t sort_tmp = 0;
+    if (lb > 0)
+        HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(nullptr, sort_tmp, (const Key*)nullptr, (Key*)nullptr,
+                                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, n,
+                                                           (unsigned)(bits - lb), (unsigned)bits, e->stream));
     const size_t b_keys = al256((size_t)n * sizeof(Key)), b_ord = al256((size_t)n * 4);
-    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, b_keys + b_ord + 256)) return rc;
+    const size_t need = b_keys + b_ord + 256 + (lb > 0 ? b_keys + 2 * b_ord + al256(sort_tmp) : 0);
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, need)) return rc;
     char* b = e->bst;
     Key* keys = (Key*)b; b += b_keys;
     uint32_t* nxt = (uint32_t*)b; b += b_ord;
-    unsigned int* flags = (unsigned int*)b;
+    unsigned int* flags = (unsigned int*)b; b += 256;
     const bool tb = e->p.mode == RAFT_MODE_TEXTBOOK;
     HIP_TRY(hipMemsetAsync(flags, 0, 12, e->stream));
     const unsigned grid = (unsigned)((n + BLOCK - 1) / BLOCK);
-    batch_claim_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, keys, e->claim, nxt, flags);
-    using AK = void (*)(DevParams, uint32_t, int, const Key*, uint2*, const uint32_t*, const void*, void*, unsigned int*);
+    uint32_t* ord = lb > 0 ? (uint32_t*)(b + b_keys) : nullptr;
+    batch_claim_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, keys, e->claim, nxt, ord, flags);
+    const Key* akeys = keys;
+    const uint32_t* aord = nullptr;
+    if (lb > 0) {
+        Key* k_out = (Key*)b; b += b_keys;
+        b += b_ord;                                // ord (the sort's input values)
+        uint32_t* o_out = (uint32_t*)b; b += b_ord;
+        HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(b, sort_tmp, keys, k_out, ord, o_out, n,
+                                                           (unsigned)(bits - lb), (unsigned)bits, e->stream));
+        akeys = k_out;
+        aord = o_out;
+    }
+    using AK = void (*)(DevParams, uint32_t, int, const Key*, const uint32_t*, uint2*, const uint32_t*, const void*,
+                        void*, unsigned int*);
     AK ak = kind == BATCH_VOTE     ? (tb ? batch_apply_kernel<true, Key, BATCH_VOTE> : batch_apply_kernel<false, Key, BATCH_VOTE>)
             : kind == BATCH_APPEND ? (tb ? batch_apply_kernel<true, Key, BATCH_APPEND> : batch_apply_kernel<false, Key, BATCH_APPEND>)
                                    : (tb ? batch_apply_kernel<true, Key, BATCH_COMMAND> : batch_apply_kernel<false, Key, BATCH_COMMAND>);
-    ak<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, keys, e->claim, nxt, req, resp, flags);
+    ak<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, akeys, aord, e->claim, nxt, req, resp, flags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 12, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -2051,12 +2096,12 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
     // runs longer than RUN_MAX: their messages sorted by (key, batch index),
     // every other message keyed `none` (sorted last and skipped)
     const Key none = (Key)e->dp.GR;
-    int bits = 1;
-    while (bits < (int)(8 * sizeof(Key)) && ((uint64_t)none >> bits)) ++bits;
-    size_t sort_tmp = 0;
+    int nbits = 1;
+    while (nbits < (int)(8 * sizeof(Key)) && ((uint64_t)none >> nbits)) ++nbits;
+    sort_tmp = 0;
     HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(nullptr, sort_tmp, (const Key*)nullptr, (Key*)nullptr,
                                                        (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u,
-                                                       (unsigned)bits, e->stream));
+                                                       (unsigned)nbits, e->stream));
     if (int rc = grow_dev(e, &e->bst2, &e->bst2_bytes, 2 * b_keys + 2 * b_ord + al256(sort_tmp))) return rc;
     b = e->bst2;
     Key* k_in = (Key*)b; b += b_keys;
@@ -2064,7 +2109,7 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
     uint32_t* o_in = (uint32_t*)b; b += b_ord;
     uint32_t* o_out = (uint32_t*)b; b += b_ord;
     batch_long_keys_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(keys, e->claim, n, none, k_in, o_in);
-    HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(b, sort_tmp, k_in, k_out, o_in, o_out, n, 0u, (unsigned)bits,
+    HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(b, sort_tmp, k_in, k_out, o_in, o_out, n, 0u, (unsigned)nbits,
                                                        e->stream));
     using BK = void (*)(DevParams, uint32_t, int, Key, const Key*, const uint32_t*, uint2*, const void*, void*,
                         unsigned int*);
