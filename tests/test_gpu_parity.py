@@ -376,6 +376,32 @@ def test_reset_then_general_kernel_equals_fresh_engine(cfg):
     f.close()
 
 
+def test_traffic_probe_changes_nothing():
+    """raft_engine_traffic_probe (the rocprofv3 calibration dispatches) moves
+    exactly the bytes it reports and changes no result: the state probe writes
+    every value back unchanged, the log-store probe writes only past physLen
+    (never read, not in the digest); the engine then steps on to the oracle's
+    counters and digest."""
+    kw = dict(abi.CONFIGS[3], G=2000, churn_ppm=20_000)
+    e, o = pair(log_cap=96, **kw)
+    ce = e.step(40)
+    co = o.step(40, nthreads=NTHREADS)[:, : abi.NUM_COUNTERS]
+    assert np.array_equal(ce, co)
+    d0, s0 = e.digest(), e.read_state()
+    state = kw["G"] * (5 * (4 * 13 + 8) + 12)
+    assert e.traffic_probe(0) == (state, state)
+    phys = s0[:, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(5)]]
+    assert e.traffic_probe(1) == (4 * kw["G"] * 5, 8 * int(np.count_nonzero(phys < 96)))
+    assert e.digest() == d0 and np.array_equal(e.read_state(), s0)
+    ce = e.step(40)
+    co = o.step(40, nthreads=NTHREADS)[:, : abi.NUM_COUNTERS]
+    assert np.array_equal(ce, co) and e.digest() == o.digest()
+    w = RaftEngine(abi.make_params(log_cap=128, log_window=64, **kw))
+    with pytest.raises(eng_mod.RaftError):
+        w.traffic_probe(1)                                # a ring has no slot past its last entry to spare
+    w.close()
+
+
 def test_shard_invariance():
     """Config 4's contract: sharding by global group id does not change any group."""
     kw = dict(abi.CONFIGS[3])
