@@ -35,6 +35,8 @@ case $P in
       step ubench 200 scripts/ubench/valu_rate3
       # the handler batches: kernel trace of the claim path, and of the sorted path (rev d93a3b4)
       step htrace 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace -o run --output-format csv -- python scripts/handler_probe.py
+      RAFT_BATCH_LOCALITY_BITS=0 step htrace_claim 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_claim -o run --output-format csv -- python scripts/handler_probe.py
+      RAFT_BATCH_LOCALITY_BITS=16 step htrace_loc16 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_loc16 -o run --output-format csv -- python scripts/handler_probe.py
       RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_sorted.so step htrace_sorted 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_sorted -o run --output-format csv -- python scripts/handler_probe.py
       TAG=r5_b_d20 step phase_d20 900 bash scripts/phase_budget.sh
       TAG=r5_b_def ARGS=" " step phase_def 900 bash scripts/phase_budget.sh
