@@ -11,7 +11,6 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -867,69 +866,41 @@ struct BatchCounters {
 
 // The batch path on the device (raft_*_batch, raft_*_batch_dev).  Messages
 // to one (group, replica) must be applied in batch order, and messages to
-// different replicas are independent.  No sort in the common case:
-//  * batch_claim_kernel: each message computes its key g * R + d (one outside
-//    the engine sets flags[0]) and claims its replica's word of the engine's
-//    claim array {count, head}: count += 1, head <- the message's index, the
-//    previous head saved in nxt[m].  The messages of one replica thus form a
-//    chain from head through nxt, `count` long.
-//  * batch_apply_kernel: one thread per message; the replica's head message
-//    (exactly one per replica) is its run's leader: it walks the chain into
-//    registers, sorts the indices into batch order, loads the replica once,
-//    applies the run with the step kernel's own handlers, stores it back and
-//    resets the count.  A random batch of 10^6 messages over 5 * 10^6
-//    replicas is ~82 % runs of one, ~16 % of two.
-//  * A run longer than RUN_MAX (flags[2]) is left for the sorted path: a
-//    stable radix sort of (key, message index) over the long runs' messages
-//    only, then one thread per sorted position, the first of each run
-//    applying it (batch_kernel).
-// The claim array is kept zero between batches: every run's leader (or the
-// sorted path) resets its count, also when flags[0] cancels the batch.
-// Key: uint32_t while G * R < 2^32 - 1, else uint64_t; the largest value is
-// the "no replica" key of a message outside the engine.
-constexpr int RUN_MAX = 64;
-
-// The locality pass of the claim path: a stable radix sort of (key, message
-// index) over the key's top LOCALITY_BITS bits only (one onesweep pass), so
-// that the handler threads of a workgroup touch a narrow range of replicas
-// and share cache lines of the field arrays (batch order within a replica is
-// kept by the claim chains, not by the sort).  Batches below LOCALITY_MIN
-// messages skip it.  RAFT_BATCH_LOCALITY_BITS (environment, read at create;
-// tuning) overrides the width, 0 disables the pass.
-constexpr int LOCALITY_BITS = 8;
-constexpr int LOCALITY_MIN = 1 << 16;
-constexpr int RUN_REG = 4;                     // runs this short sort in registers
-
+// different replicas are independent.  batch_keys_kernel turns each message
+// into its key g * R + d (a message outside the engine sets flags[0]); a
+// stable radix sort of (key, message index) then puts each replica's messages
+// next to each other in batch order, and batch_kernel runs one thread per
+// sorted position: the first position of each key's run loads that replica,
+// applies the run's messages in order and stores it back.
+// Key: uint32_t while G * R fits (half the sort's key traffic), else uint64_t.
 template <class Key>
-__global__ __launch_bounds__(BLOCK) void batch_claim_kernel(const int64_t* __restrict__ group,
-                                                            const int32_t* __restrict__ dst, int n, int64_t G, int R,
-                                                            Key* __restrict__ keys, uint2* __restrict__ claim,
-                                                            uint32_t* __restrict__ nxt, uint32_t* __restrict__ ord,
-                                                            unsigned int* flags) {
+__global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __restrict__ group,
+                                                           const int32_t* __restrict__ dst, int n, int64_t G, int R,
+                                                           Key* __restrict__ keys, uint32_t* __restrict__ ord,
+                                                           unsigned int* flags) {
     const int m = blockIdx.x * BLOCK + threadIdx.x;
     if (m >= n) return;
-    if (ord) ord[m] = (uint32_t)m;                                      // the locality sort's values
     const int64_t g = group[m];
     const int32_t d = dst[m];
-    if (!(g >= 0 && g < G && d >= 0 && d < R)) {
-        keys[m] = ~(Key)0;
-        atomicOr(&flags[0], 1u);
-        return;
-    }
-    const Key key = (Key)((uint64_t)g * (uint64_t)R + (uint64_t)d);
-    keys[m] = key;
-    uint32_t* const w = (uint32_t*)&claim[key];
-    __hip_atomic_fetch_add(&w[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    nxt[m] = __hip_atomic_exchange(&w[1], (uint32_t)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool ok = g >= 0 && g < G && d >= 0 && d < R;
+    keys[m] = ok ? (Key)((uint64_t)g * (uint64_t)R + (uint64_t)d) : (Key)0;
+    ord[m] = (uint32_t)m;
+    if (!ok) atomicOr(&flags[0], 1u);
 }
 
-// Apply the c messages ids(0..c-1) (batch order) to replica idx = g * R + r:
-// one load of the replica, the reference's handler per message, one store.
-// flags[1]: accesses below the retained log window (RAFT_EWINDOW).
-template <bool TB, int kind, class Ids>
-__device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_t idx, Ids ids, int c, const void* req,
-                                          void* resp, unsigned int* flags) {
+// flags[0]: a message was outside the engine (nothing is applied);
+// flags[1]: accesses below the retained log window (RAFT_EWINDOW)
+template <bool TB, class Key, int kind>
+__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int n,
+                                                      const Key* __restrict__ keys,
+                                                      const uint32_t* __restrict__ order, const void* req, void* resp,
+                                                      unsigned int* flags) {
+    const int m0 = blockIdx.x * BLOCK + threadIdx.x;
+    if (m0 >= n || *(volatile unsigned int*)&flags[0]) return;
+    const Key key = keys[m0];
+    if (m0 > 0 && keys[m0 - 1] == key) return;                          // not the first of its run
     const int R = p.R;
+    const int64_t idx = (int64_t)key;
     const int64_t i = idx / R;
     const int r = (int)(idx - i * R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
@@ -941,8 +912,8 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
     derive_cache<VO>(x, lv);
     BatchCounters cnt;
     bool drew = false;
-    for (int k = 0; k < c; ++k) {
-        const uint32_t o = ids(k);
+    for (int m = m0; m < n && keys[m] == key; ++m) {
+        const uint32_t o = order[m];
         if constexpr (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
@@ -972,101 +943,6 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
     }
     store_rep<VO>(x, o, drew, p, idx);
     if (cnt.miss) atomicAdd(&flags[1], cnt.miss);
-}
-
-// One thread per message; the run's leader (the replica's head) applies it.
-// flags[0]: a message was outside the engine, nothing is applied (the counts
-// are still reset); flags[2]: a run longer than RUN_MAX, left to the sorted
-// path with its count in place.
-template <bool TB, class Key, int kind>
-__global__ __launch_bounds__(BLOCK) void batch_apply_kernel(DevParams p, uint32_t t, int n,
-                                                            const Key* __restrict__ keys,
-                                                            const uint32_t* __restrict__ order,
-                                                            uint2* __restrict__ claim,
-                                                            const uint32_t* __restrict__ nxt, const void* req,
-                                                            void* resp, unsigned int* flags) {
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    // order (nullable): the messages partially sorted by replica, so that
-    // neighbouring threads touch neighbouring replicas' fields; keys[i] is
-    // then the key of message order[i]
-    const int m = order ? (int)order[i] : i;
-    const Key key = keys[i];
-    if (key == ~(Key)0) return;                                         // outside the engine
-    const uint2 w = claim[key];
-    if (w.y != (uint32_t)m) return;                                     // not its run's leader
-    const int c = (int)w.x;
-    if (*(volatile unsigned int*)&flags[0]) {                           // the batch is refused
-        claim[key].x = 0u;
-        return;
-    }
-    if (c == 1) {                                                       // alone on its replica (common)
-        apply_run<TB, kind>(p, t, (int64_t)key, [m](int) { return (uint32_t)m; }, 1, req, resp, flags);
-    } else if (c <= RUN_REG) {
-        // the chain from the head is in reverse claim order: into registers,
-        // then a sorting network into batch order
-        uint32_t v[RUN_REG];
-        v[0] = (uint32_t)m;
-#pragma unroll
-        for (int k = 1; k < RUN_REG; ++k) v[k] = k < c ? nxt[v[k - 1]] : 0xFFFFFFFFu;
-#pragma unroll
-        for (int a = 0; a < RUN_REG; ++a)
-#pragma unroll
-            for (int b = RUN_REG - 1; b > a; --b) {
-                const uint32_t lo = min(v[b - 1], v[b]), hi = max(v[b - 1], v[b]);
-                v[b - 1] = lo;
-                v[b] = hi;
-            }
-        apply_run<TB, kind>(p, t, (int64_t)key, [&v](int k) {
-            uint32_t x = v[0];
-#pragma unroll
-            for (int q = 1; q < RUN_REG; ++q) x = k == q ? v[q] : x;
-            return x;
-        }, c, req, resp, flags);
-    } else if (c <= RUN_MAX) {
-        uint32_t v[RUN_MAX];                                            // private memory (rare)
-        v[0] = (uint32_t)m;
-        for (int k = 1; k < c; ++k) v[k] = nxt[v[k - 1]];
-        for (int a = 1; a < c; ++a) {                                   // insertion sort
-            const uint32_t x = v[a];
-            int b = a - 1;
-            for (; b >= 0 && v[b] > x; --b) v[b + 1] = v[b];
-            v[b + 1] = x;
-        }
-        apply_run<TB, kind>(p, t, (int64_t)key, [&v](int k) { return v[k]; }, c, req, resp, flags);
-    } else {
-        atomicOr(&flags[2], 1u);
-        return;
-    }
-    claim[key].x = 0u;
-}
-
-// The sorted path for the runs longer than RUN_MAX: their messages get their
-// key, every other message the key G * R (sorted last, skipped).
-template <class Key>
-__global__ __launch_bounds__(BLOCK) void batch_long_keys_kernel(const Key* __restrict__ keys,
-                                                                const uint2* __restrict__ claim, int n, Key none,
-                                                                Key* __restrict__ out, uint32_t* __restrict__ ord) {
-    const int m = blockIdx.x * BLOCK + threadIdx.x;
-    if (m >= n) return;
-    const Key key = keys[m];
-    out[m] = key != ~(Key)0 && (int)claim[key].x > RUN_MAX ? key : none;
-    ord[m] = (uint32_t)m;
-}
-
-template <bool TB, class Key, int kind>
-__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int n, Key none,
-                                                      const Key* __restrict__ keys,
-                                                      const uint32_t* __restrict__ order, uint2* __restrict__ claim,
-                                                      const void* req, void* resp, unsigned int* flags) {
-    const int m0 = blockIdx.x * BLOCK + threadIdx.x;
-    if (m0 >= n) return;
-    const Key key = keys[m0];
-    if (key == none || (m0 > 0 && keys[m0 - 1] == key)) return;        // not the first of a long run
-    int c = 1;
-    while (m0 + c < n && keys[m0 + c] == key) ++c;
-    apply_run<TB, kind>(p, t, (int64_t)key, [order, m0](int k) { return order[m0 + k]; }, c, req, resp, flags);
-    claim[key].x = 0u;
 }
 
 // read_log / write_log: the host's [n][R][log_cap] image of groups [g0, g0+n)
@@ -1131,13 +1007,8 @@ struct raft_engine {
     bool fork_needed;           // the engine stream holds work the sub-range streams have not waited for
     // batch path staging, grow-only: device scratch (keys, sort), device
     // copies of host batches, pinned host staging, pinned status flags
-    char* bst;                  // claim-path scratch: keys, chain links, flags
+    char* bst;
     size_t bst_bytes;
-    char* bst2;                 // sorted-path scratch (runs longer than RUN_MAX)
-    size_t bst2_bytes;
-    uint2* claim;               // [G * R] {count, head} per replica, zero between batches
-    size_t claim_bytes;
-    int locality_bits;          // the claim path's locality sort (LOCALITY_BITS; 0 = none)
     char* bio;
     size_t bio_bytes;
     char* hst;
@@ -1405,12 +1276,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->ev_wait = nullptr;
     for (int q = 0; q < RAFT_MAX_SUBRANGES; ++q) { e->sub_stream[q] = nullptr; e->ev_sub_done[q] = nullptr; }
     e->ev_red_done[0] = e->ev_red_done[1] = nullptr;
-    e->bst = e->bst2 = e->bio = e->hst = nullptr;
-    e->bst_bytes = e->bst2_bytes = e->bio_bytes = e->hst_bytes = 0;
-    e->claim = nullptr;
-    e->claim_bytes = 0;
-    e->locality_bits = LOCALITY_BITS;
-    if (const char* lbv = std::getenv("RAFT_BATCH_LOCALITY_BITS")) e->locality_bits = std::max(0, std::atoi(lbv));
+    e->bst = e->bio = e->hst = nullptr;
+    e->bst_bytes = e->bio_bytes = e->hst_bytes = 0;
     e->bflags_host = nullptr;
     e->aux = nullptr;
     e->aux_bytes = 0;
@@ -1555,8 +1422,6 @@ int raft_engine_destroy(raft_engine* e) {
     for (hipEvent_t x : {e->ev_fork, e->ev_red_done[0], e->ev_red_done[1], e->ev_wait})
         if (x) (void)hipEventDestroy(x);
     if (e->bst) (void)hipFree(e->bst);
-    if (e->bst2) (void)hipFree(e->bst2);
-    if (e->claim) (void)hipFree(e->claim);
     if (e->bio) (void)hipFree(e->bio);
     if (e->hst) (void)hipHostFree(e->hst);
     if (e->bflags_host) (void)hipHostFree(e->bflags_host);
@@ -1819,21 +1684,18 @@ int raft_engine_set_step_index(raft_engine* e, int64_t t) {
     return RAFT_OK;
 }
 int64_t raft_engine_device_bytes(raft_engine* e) {
-    return e ? (int64_t)(e->bytes + e->bst_bytes + e->bst2_bytes + e->claim_bytes + e->bio_bytes + e->aux_bytes) : -1;
+    return e ? (int64_t)(e->bytes + e->bst_bytes + e->bio_bytes + e->aux_bytes) : -1;
 }
 int raft_engine_trim_staging(raft_engine* e) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->bst) HIP_TRY(hipFree(e->bst));
-    if (e->bst2) HIP_TRY(hipFree(e->bst2));
-    if (e->claim) HIP_TRY(hipFree(e->claim));
     if (e->bio) HIP_TRY(hipFree(e->bio));
     if (e->aux) HIP_TRY(hipFree(e->aux));
     if (e->hst) HIP_TRY(hipHostFree(e->hst));
-    e->bst = e->bst2 = e->bio = e->aux = e->hst = nullptr;
-    e->claim = nullptr;
-    e->bst_bytes = e->bst2_bytes = e->claim_bytes = e->bio_bytes = e->aux_bytes = e->hst_bytes = 0;
+    e->bst = e->bio = e->aux = e->hst = nullptr;
+    e->bst_bytes = e->bio_bytes = e->aux_bytes = e->hst_bytes = 0;
     return RAFT_OK;
 }
 
@@ -2033,107 +1895,51 @@ int raft_engine_check_log_matching(raft_engine* e, int64_t g0, int64_t n, uint8_
 // pass and one pass per 8 key bits).
 using BatchSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                    rocprim::default_config, 0>;
-
-// The engine's claim array (one {count, head} word per replica, zero between
-// batches): allocated and zeroed at the first batch, released by
-// raft_engine_trim_staging.
-static int ensure_claim(raft_engine* e) {
-    if (e->claim) return RAFT_OK;
-    const size_t b = (size_t)e->dp.GR * sizeof(uint2);
-    HIP_TRY(hipMalloc((void**)&e->claim, b));
-    e->claim_bytes = b;
-    HIP_TRY(hipMemsetAsync(e->claim, 0, b, e->stream));
-    return RAFT_OK;
-}
-
-
 extern "C++" template <class Key>
 static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
-                          void* resp, int n) {
+                          void* resp, int n, int bits) {
     const int R = e->p.R;
-    if (int rc = ensure_claim(e)) return rc;
-    int bits = 1;                                 // key bits; the outside-the-engine key ~0 sorts last
-    while (bits < (int)(8 * sizeof(Key)) && (((uint64_t)e->dp.GR - 1) >> bits)) ++bits;
-    const int lb = n >= LOCALITY_MIN ? std::min(e->locality_bits, bits) : 0;
     size_t sort_tmp = 0;
-    if (lb > 0)
-        HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(nullptr, sort_tmp, (const Key*)nullptr, (Key*)nullptr,
-                                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, n,
-                                                           (unsigned)(bits - lb), (unsigned)bits, e->stream));
-    const size_t b_keys = al256((size_t)n * sizeof(Key)), b_ord = al256((size_t)n * 4);
-    const size_t need = b_keys + b_ord + 256 + (lb > 0 ? b_keys + 2 * b_ord + al256(sort_tmp) : 0);
-    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, need)) return rc;
-    char* b = e->bst;
-    Key* keys = (Key*)b; b += b_keys;
-    uint32_t* nxt = (uint32_t*)b; b += b_ord;
-    unsigned int* flags = (unsigned int*)b; b += 256;
-    const bool tb = e->p.mode == RAFT_MODE_TEXTBOOK;
-    HIP_TRY(hipMemsetAsync(flags, 0, 12, e->stream));
-    const unsigned grid = (unsigned)((n + BLOCK - 1) / BLOCK);
-    uint32_t* ord = lb > 0 ? (uint32_t*)(b + b_keys) : nullptr;
-    batch_claim_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, keys, e->claim, nxt, ord, flags);
-    const Key* akeys = keys;
-    const uint32_t* aord = nullptr;
-    if (lb > 0) {
-        Key* k_out = (Key*)b; b += b_keys;
-        b += b_ord;                                // ord (the sort's input values)
-        uint32_t* o_out = (uint32_t*)b; b += b_ord;
-        HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(b, sort_tmp, keys, k_out, ord, o_out, n,
-                                                           (unsigned)(bits - lb), (unsigned)bits, e->stream));
-        akeys = k_out;
-        aord = o_out;
-    }
-    using AK = void (*)(DevParams, uint32_t, int, const Key*, const uint32_t*, uint2*, const uint32_t*, const void*,
-                        void*, unsigned int*);
-    AK ak = kind == BATCH_VOTE     ? (tb ? batch_apply_kernel<true, Key, BATCH_VOTE> : batch_apply_kernel<false, Key, BATCH_VOTE>)
-            : kind == BATCH_APPEND ? (tb ? batch_apply_kernel<true, Key, BATCH_APPEND> : batch_apply_kernel<false, Key, BATCH_APPEND>)
-                                   : (tb ? batch_apply_kernel<true, Key, BATCH_COMMAND> : batch_apply_kernel<false, Key, BATCH_COMMAND>);
-    ak<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, akeys, aord, e->claim, nxt, req, resp, flags);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 12, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    if (!e->bflags_host[2]) return RAFT_OK;
-    // runs longer than RUN_MAX: their messages sorted by (key, batch index),
-    // every other message keyed `none` (sorted last and skipped)
-    const Key none = (Key)e->dp.GR;
-    int nbits = 1;
-    while (nbits < (int)(8 * sizeof(Key)) && ((uint64_t)none >> nbits)) ++nbits;
-    sort_tmp = 0;
     HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(nullptr, sort_tmp, (const Key*)nullptr, (Key*)nullptr,
                                                        (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u,
-                                                       (unsigned)nbits, e->stream));
-    if (int rc = grow_dev(e, &e->bst2, &e->bst2_bytes, 2 * b_keys + 2 * b_ord + al256(sort_tmp))) return rc;
-    b = e->bst2;
+                                                       (unsigned)bits, e->stream));
+    const size_t b_keys = al256((size_t)n * sizeof(Key)), b_ord = al256((size_t)n * 4);
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, 2 * b_keys + 2 * b_ord + al256(sort_tmp) + 256)) return rc;
+    char* b = e->bst;
     Key* k_in = (Key*)b; b += b_keys;
     Key* k_out = (Key*)b; b += b_keys;
     uint32_t* o_in = (uint32_t*)b; b += b_ord;
     uint32_t* o_out = (uint32_t*)b; b += b_ord;
-    batch_long_keys_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(keys, e->claim, n, none, k_in, o_in);
-    HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(b, sort_tmp, k_in, k_out, o_in, o_out, n, 0u, (unsigned)nbits,
+    unsigned int* flags = (unsigned int*)b; b += 256;
+    void* tmp = b;
+    HIP_TRY(hipMemsetAsync(flags, 0, 8, e->stream));
+    const unsigned grid = (unsigned)((n + BLOCK - 1) / BLOCK);
+    batch_keys_kernel<Key><<<grid, BLOCK, 0, e->stream>>>(group, dst, n, e->p.G, R, k_in, o_in, flags);
+    HIP_TRY(rocprim::radix_sort_pairs<BatchSortConfig>(tmp, sort_tmp, k_in, k_out, o_in, o_out, n, 0u, (unsigned)bits,
                                                        e->stream));
-    using BK = void (*)(DevParams, uint32_t, int, Key, const Key*, const uint32_t*, uint2*, const void*, void*,
-                        unsigned int*);
+    using BK = void (*)(DevParams, uint32_t, int, const Key*, const uint32_t*, const void*, void*, unsigned int*);
+    const bool tb = e->p.mode == RAFT_MODE_TEXTBOOK;
     BK kern = kind == BATCH_VOTE     ? (tb ? batch_kernel<true, Key, BATCH_VOTE> : batch_kernel<false, Key, BATCH_VOTE>)
               : kind == BATCH_APPEND ? (tb ? batch_kernel<true, Key, BATCH_APPEND> : batch_kernel<false, Key, BATCH_APPEND>)
                                      : (tb ? batch_kernel<true, Key, BATCH_COMMAND> : batch_kernel<false, Key, BATCH_COMMAND>);
-    kern<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, none, k_out, o_out, e->claim, req, resp, flags);
+    kern<<<grid, BLOCK, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, k_out, o_out, req, resp, flags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return RAFT_OK;
 }
 
-// The batch on device buffers: claims, the handlers (a sort only for runs
-// longer than RUN_MAX); one synchronisation at the end for the status flags.
+// The batch on device buffers: keys, a stable radix sort over the key bits,
+// the handlers; one synchronisation at the end for the status flags.
 static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
                          void* resp, int64_t n64) {
     e->fork_needed = true;
     const int n = (int)n64;
     const uint64_t nkeys = (uint64_t)e->p.G * (uint64_t)e->p.R;
-    // 32-bit keys while every key and the two reserved values (`none` = G * R
-    // of the sorted path, ~0 = outside the engine) fit
-    const int rc = nkeys < 0xFFFFFFFFull ? run_batch_keys<uint32_t>(e, kind, group, dst, req, resp, n)
-                                         : run_batch_keys<uint64_t>(e, kind, group, dst, req, resp, n);
+    int bits = 1;
+    while (bits < 64 && (nkeys - 1) >> bits) ++bits;
+    const int rc = bits <= 32 ? run_batch_keys<uint32_t>(e, kind, group, dst, req, resp, n, bits)
+                              : run_batch_keys<uint64_t>(e, kind, group, dst, req, resp, n, bits);
     if (rc) return rc;
     e->cache_valid = false;
     if (e->bflags_host[0]) return fail(RAFT_ERANGE, "a message's group or replica index is outside the engine; "
