@@ -41,6 +41,9 @@ constexpr int BLOCK = 256;
 #ifdef RAFT_PROFILE_PHASES
 __device__ unsigned long long g_phase_cycles[PH_N];   // diagnostic builds only
 #endif
+#ifdef RAFT_BRANCH_STATS
+__device__ unsigned long long g_branch_stats[BS_N];   // diagnostic builds only (raft_step.h BSTAT)
+#endif
 #ifdef RAFT_WAVE_TIMES
 // diagnostic builds only: per wave of the last step launch, its start and end
 // (s_memrealtime, 100 MHz, chip-wide) and its HW_ID / XCC_ID registers
@@ -385,6 +388,9 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     c.jl = lds + wib * 256;
     c.tl = lds + JOB_LDS_WORDS + wib * 16;
     c.clk.start();
+#ifdef RAFT_BRANCH_STATS
+    for (int q = 0; q < BS_N; ++q) c.bs[q] = 0;
+#endif
     Node n;
     // One loop over the wave's chunk-steps; a piece boundary (the launch's
     // end in the one-chunk-per-wave schedule) is a rare branch in it that
@@ -489,6 +495,10 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
 #ifdef RAFT_PROFILE_PHASES
     if (lane == 0)
         for (int q = 0; q < PH_N; ++q) atomicAdd(&g_phase_cycles[q], (unsigned long long)c.clk.acc[q]);
+#endif
+#ifdef RAFT_BRANCH_STATS
+    if (lane == 0)
+        for (int q = 0; q < BS_N; ++q) atomicAdd(&g_branch_stats[q], (unsigned long long)c.bs[q]);
 #endif
 #ifdef RAFT_WAVE_TIMES
     {
@@ -1394,6 +1404,23 @@ int raft_engine_destroy(raft_engine* e) {
             fprintf(stderr, "[phase-cycles]");
             for (int q = 0; q < PH_N; ++q) fprintf(stderr, " %s=%.1f%%", names[q], tot ? 100.0 * v[q] / tot : 0.0);
             fprintf(stderr, " total=%llu\n", tot);
+        }
+    }
+#endif
+#ifdef RAFT_BRANCH_STATS
+    {   // per wave-step frequency of each branch over the engine's step launches, to stderr
+        unsigned long long v[BS_N] = {0};
+        (void)hipSetDevice(e->device);
+        (void)hipStreamSynchronize(e->stream);
+        if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_branch_stats), sizeof(v)) == hipSuccess) {
+            const char* names[BS_N] = {"steps", "T_busy", "V_phase", "V_rounds", "V_stage", "D_dec", "D_backoff",
+                                       "D_start", "A_phase", "A_rounds", "A_stage", "A_swap", "A_loads", "A_hib",
+                                       "A_slow", "A_commit", "H_busy", "K_dual", "draw", "direct_drop"};
+            fprintf(stderr, "[branch-stats] wave_steps=%llu", v[0]);
+            for (int q = 1; q < BS_N; ++q) fprintf(stderr, " %s=%.4f", names[q], v[0] ? (double)v[q] / v[0] : 0.0);
+            fprintf(stderr, "\n");
+            unsigned long long z[BS_N] = {0};
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_branch_stats), z, sizeof(z));
         }
     }
 #endif

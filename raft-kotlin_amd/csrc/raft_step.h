@@ -293,6 +293,19 @@ struct PhaseClock {
 #endif
 };
 
+// Branch statistics (diagnostic builds only, -DRAFT_BRANCH_STATS): how often
+// each wave-uniform branch of the step runs, per wave, added into a global
+// array at the end of the launch (raft_engine.hip prints it at destroy).
+// Never compiled into the product build.
+enum { BS_STEPS = 0, BS_T_BUSY, BS_V_PHASE, BS_V_ROUNDS, BS_V_STAGE, BS_D_DEC, BS_D_BACKOFF, BS_D_START,
+       BS_A_PHASE, BS_A_ROUNDS, BS_A_STAGE, BS_A_SWAP, BS_A_LOADS, BS_A_HIB, BS_A_SLOW, BS_A_COMMIT,
+       BS_H_BUSY, BS_K_DUAL, BS_DRAW, BS_DIRECT_DROP, BS_N };
+#ifdef RAFT_BRANCH_STATS
+#define BSTAT(c, i) ((c).bs[i] += 1u)
+#else
+#define BSTAT(c, i) ((void)0)
+#endif
+
 // Phase budget (diagnostic builds only, -DRAFT_PHASE_TWICE=1 + PH_x): phase
 // x runs a second time first, on copies of the node, context and counters
 // whose results are sunk, so SQ_INSTS_VALU / SALU of that build minus the
@@ -616,6 +629,9 @@ struct Ctx {
     uint32_t lead;            // the group's LEADER bits at the end of the last step (loop-carried)
     uint32_t tw, dwt, dwv;    // this lane's timer word and prefetched tick / vote drop words
     PhaseClock clk;
+#ifdef RAFT_BRANCH_STATS
+    uint32_t bs[BS_N];
+#endif
     int s_tick, s_vote;       // senders whose drop words the jobs hold (-1 none)
     uint2* lr;                // this replica's log row: slot 0 (its wave's block, its lane)
 
@@ -693,7 +709,7 @@ __device__ __forceinline__ uint32_t job_word(const Ctx<R>& c, int first_job, int
 }
 
 template <int R, bool HAVE_JOB, int NET>
-__device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& c, uint32_t purpose, uint64_t act,
+__device__ __forceinline__ uint32_t drop_word(const DevParams& p, Ctx<R>& c, uint32_t purpose, uint64_t act,
                                               int s, uint32_t prefetched, int s_job) {
     if (drops_off<NET>(p)) return 0u;
     uint32_t w = 0;
@@ -703,6 +719,7 @@ __device__ __forceinline__ uint32_t drop_word(const DevParams& p, const Ctx<R>& 
         need = act & lm(s != s_job);
     }
     if (RARE(need)) {
+        BSTAT(c, BS_DIRECT_DROP);
         if (ib(need)) w = drop_word_direct(p, c, purpose, s);
     }
     return w;
@@ -801,6 +818,7 @@ struct Stepper {
     __device__ __forceinline__ static void tick(const DevParams& p, Ctx<R>& c, Node& n, uint64_t mtk, int s,
                                                 uint32_t fs, Counters& cnt) {
         const int sl = c.src(s);
+        BSTAT(c, BS_A_ROUNDS);
         // the leader's tick-start snapshot and this destination's drop word,
         // all cross-lane reads issued together (one LDS round trip)
         const int32_t role_s = bcast(n.role, sl);
@@ -817,6 +835,7 @@ struct Stepper {
         cnt.add(run & mme, RAFT_C_SESSIONS_TICKED);
         const uint64_t swap = run & lm(n.s0 != s);                        // swap the session in (rare)
         if (RARE(swap)) {
+            BSTAT(c, BS_A_SWAP);
             if (ib(swap)) {
                 if (n.s0 >= 0) spill_store(p, c, n, n.s0);
                 spill_load(p, c, n, s);
@@ -859,6 +878,7 @@ struct Stepper {
         const uint64_t ld3 = ok & p0 & lm(prev < n.last - 2);
         const uint64_t ld4 = TB ? ok & has & lm(prev + 1 < n.last - 2) : 0ull;
         if (ld1 | ld2 | ld3 | ld4) {                                      // rare: tail-cache misses
+            BSTAT(c, BS_A_LOADS);
             if (ib(ld1)) lpt = (int32_t)ls.template at<RING>(prev)->x;
             if (ib(ld2)) lent = *ls.template at<RING>(i - 1);
             if (ib(ld3)) dpt = (int32_t)lv.template at<RING>(prev)->x;
@@ -943,6 +963,7 @@ struct Stepper {
         const uint64_t hib = delivered & lm(rterm > Lterm);
         bool stepdown = false;
         if (RARE(hib)) {                                                  // wave-uniform, rare
+            BSTAT(c, BS_A_HIB);
             stepdown = c.gbits(hib) != 0;
             const uint32_t dl = c.gbits(delivered);
 #pragma unroll
@@ -977,6 +998,7 @@ struct Stepper {
         // count(matchIndex > commitIndex) >= majority => commitIndex += 1
         int32_t C = Lcommit;
         if (!TB && chk) {                                                 // wave-uniform
+            BSTAT(c, BS_A_COMMIT);
             const uint32_t ck = c.gbits(chk);                             // the group's acked responses
             // Closed form (common case).  While no row went down (monotone:
             // an ack raises matchIndex, a nak keeps it), the count of rows
@@ -997,6 +1019,7 @@ struct Stepper {
                 C = inc_if(C, inc);
                 cnt.add(inc & L::lanes_of(0), RAFT_C_COMMITS);            // one lane per group
             } else {
+                BSTAT(c, BS_A_SLOW);
                 // the replay in destination order.  Bit q of the group's acks,
                 // pre-shifted so that one v_bcnt adds it (as 16 << q) to the
                 // popcount: pc >= (16 << q) + MAJ tests "response q acked and
@@ -1063,6 +1086,7 @@ struct Stepper {
     // wave-uniform control flow.
     __device__ __forceinline__ static void stage_sender_chunks(const DevParams& p, Ctx<R>& c, uint32_t purpose) {
         if (drops_off<NET>(p)) return;
+        BSTAT(c, purpose == RAFT_RNG_VOTE_DROP ? BS_V_STAGE : BS_A_STAGE);
         const u32x4 w = kdraw(p, c.t, c.gid(), purpose, (uint32_t)c.r);
         *(uint4*)&c.jl[(c.base + c.r) << 2] = make_uint4(w.x, w.y, w.z, w.w);
         asm volatile("" ::: "memory");
@@ -1081,6 +1105,7 @@ struct Stepper {
         const int r = c.r;
         const int s = ib(mvr) ? __builtin_ctz(vtodo) : 0;
         vtodo &= vtodo - 1u;
+        BSTAT(c, BS_V_ROUNDS);
         const int sl = c.src(s);
         const uint32_t ms = bcastu(send, sl);                       // sender s's pending dsts
         const int32_t rt = bcast(qt, sl), rli = bcast(qli, sl), rlt = bcast(qlt, sl);
@@ -1151,6 +1176,7 @@ struct Stepper {
     // Called by all 64 lanes (converged); `n` of a dead lane is inert.
     __device__ __forceinline__ static void step(const DevParams& p, Ctx<R>& c, Node& n, Counters& cnt) {
         const int r = c.r;
+        BSTAT(c, BS_STEPS);
         // H needs the roles at step start (the lowest-id LEADER to isolate);
         // T draws no randomness, so it runs before the step's Philox pass and
         // that pass already knows the first RequestVote sender.
@@ -1177,6 +1203,7 @@ struct Stepper {
             n.elec = ib(t_armed) ? t_el : n.elec;
             send = 0u; sstart = 0; qt = qli = qlt = 0;
             if (t_fire | electing) {
+                BSTAT(c, BS_T_BUSY);
                 uint32_t f = n.fl;
                 const bool fire = ib(t_fire);
                 n.elec = fire ? 0 : n.elec;                                     // fire is within t_armed
@@ -1292,6 +1319,7 @@ struct Stepper {
             // only waves where an isolation runs or may start (~1/5) do the rest
             // (none in a kernel built without NET_ISO: no churn, no isolation word)
             if ((NET & NET_ISO) != 0 && RARE(lm(n.iso != 0) | lm((uint64_t)hw0 < churn_thr))) {
+                BSTAT(c, BS_H_BUSY);
                 const int32_t churn_steps = kp->churn_steps;
                 int32_t rem = n.iso >> 8, rep = n.iso & 0xFF;
                 if (rem > 0) { rem--; if (rem == 0) rep = 0; }
@@ -1314,6 +1342,7 @@ struct Stepper {
         // and the loop condition (one ballot per round)
         auto phase_v = [&](Ctx<R>& c, Node& n, Counters& cnt, uint32_t vtodo, uint64_t mv) {
             if (mv) {
+                BSTAT(c, BS_V_PHASE);
                 // RING: the replicas whose log.get(lastIndex - 1) is below the
                 // window; hasl: lastIndex >= 1 (the vote handlers do not touch the
                 // logs, so both hold for the whole phase)
@@ -1360,6 +1389,7 @@ struct Stepper {
                 dec = inr & (lm(latch >= MAJ) | lm(n.phase >= p.round_to));
             }
             if (dec) {                                                      // wave-uniform
+                BSTAT(c, BS_D_DEC);
                 const int votes = (f >> VOTES_SH) & 0xF;
                 const uint64_t cand = dec & lm(n.role == RAFT_CANDIDATE);
                 const uint64_t win = cand & lm(votes >= MAJ);               // :218-219
@@ -1377,10 +1407,12 @@ struct Stepper {
             }
         }
         if (need_bo) {
+            BSTAT(c, BS_D_BACKOFF);
             const uint32_t w = timer_word(p, c);
             const KernArgs kp = kernargs();
             if (ib(need_bo)) n.phase = scale_range(w, kp->bmin, kp->bmax);
         }
+        if (dstart) BSTAT(c, BS_D_START);
         start_sessions(p, c, n, dstart, cnt);
         c.clk.mark(PH_D);
 
@@ -1393,6 +1425,7 @@ struct Stepper {
         // predicate and the loop condition, one ballot per round)
         auto phase_a = [&](Ctx<R>& c, Node& n, Counters& cnt, uint32_t todo, uint64_t mt) {
             if (LIKELY(mt)) {
+                BSTAT(c, BS_A_PHASE);
                 const uint32_t fs = follower_sent(n.fl);                        // FL_ELECTING is fixed during A
                 {
                     // R = 2: the job lanes do not hold the first leader's chunk,
@@ -1448,6 +1481,7 @@ struct Stepper {
             cnt.add(isl, RAFT_C_LEADERS);
             cnt.add(glead, RAFT_C_GROUPS_WITH_LEADER);
             if (RARE(__popcll(isl) != __popcll(glead))) {                   // some group has 2+ leaders (rare)
+                BSTAT(c, BS_K_DUAL);
                 bool dual = false;
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
@@ -1463,6 +1497,7 @@ struct Stepper {
         // the deferred ResettableCountdownTimer draws of this step (S-9)
         const uint64_t dm = lm(n.fl & FL_DRAW);
         if (dm) {
+            BSTAT(c, BS_DRAW);
             const uint32_t w = timer_word(p, c);
             if (ib(dm)) {
                 const KernArgs kp = kernargs();

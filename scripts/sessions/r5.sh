@@ -41,6 +41,14 @@ case $P in
       TAG=r5_b_d20 step phase_d20 900 bash scripts/phase_budget.sh
       TAG=r5_b_def ARGS=" " step phase_def 900 bash scripts/phase_budget.sh
       ;;
+  c)  # parity suite; branch frequencies (RAFT_BRANCH_STATS build) of the driver's launch and the default
+      # bench; the driver's bench line; its PMC rows with the in-process traffic probes
+      step pytest 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+      RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_bstats.so step bstats_d20 300 python -u bench.py --steps 20 --warmup 5 $Q
+      RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_bstats.so step bstats_def 300 python -u bench.py $Q
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      TAG=r5_c_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
