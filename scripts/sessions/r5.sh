@@ -49,6 +49,13 @@ case $P in
       step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       TAG=r5_c_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       ;;
+  d)  # the short shard's timeline: kernel + HIP runtime trace of the 1/8 shard's 20-step run, plain and
+      # with the one-rank RCCL all-reduce inside the clock (scripts/trace_timeline.py)
+      step trace_s8 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $OUT/trace_s8 -o run --output-format csv -- python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step trace_s8_rccl 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $OUT/trace_s8_rccl -o run --output-format csv -- python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      python scripts/trace_timeline.py $OUT/trace_s8 > $OUT/timeline_s8.json
+      python scripts/trace_timeline.py $OUT/trace_s8_rccl > $OUT/timeline_s8_rccl.json
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
