@@ -42,9 +42,4 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" \
     [ $rc -eq 137 ] || [ $rc -eq 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ] && exit $rc
   fi
 done
-for c in FETCH_SIZE WRITE_SIZE; do
-  echo "calib $c" >> "$OUT/status.txt"
-  timeout -s KILL 120 rocprofv3 --pmc $c -d "$OUT/calib_$c" -o run --output-format csv -- \
-      python scripts/traffic_run.py calib > "$OUT/calib_$c.log" 2>&1 || exit $?
-done
 python scripts/pmc_parse.py "$OUT" && echo "parsed" >> "$OUT/status.txt"

@@ -55,6 +55,14 @@ case $P in
       RAFT_BENCH_FORCE_COLLECTIVE=1 step trace_s8_rccl 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $OUT/trace_s8_rccl -o run --output-format csv -- python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
       python scripts/trace_timeline.py $OUT/trace_s8 > $OUT/timeline_s8.json
       python scripts/trace_timeline.py $OUT/trace_s8_rccl > $OUT/timeline_s8_rccl.json
+      # row 22's upper bound: every log store sunk into one slot per wave (results differ; timing only)
+      for i in 1 2; do
+        step ab_prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_sink.so step ab_sink_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        step ab_prod_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_sink.so step ab_sink_def_$i 200 python -u bench.py $Q
+      done
+      for f in $OUT/ab_*.log; do echo "$(basename $f) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"value": [0-9.e+]*' $f | head -1)"; done > $OUT/ab_summary.txt
       ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
