@@ -64,6 +64,25 @@ case $P in
       done
       for f in $OUT/ab_*.log; do echo "$(basename $f) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"value": [0-9.e+]*' $f | head -1)"; done > $OUT/ab_summary.txt
       ;;
+  e)  # A/B of kernel variants (VARIANTS, built by scripts/build_variants.sh): dynamic VALU / SALU per
+      # chunk-step (SQ_INSTS_* of the last step launch) and interleaved timings, driver's launch and default
+      for v in prod ${VARIANTS:-}; do
+        lib=$PWD/raft-kotlin_amd/lib/libraft_engine_$v.so; [ $v = prod ] && lib=$PWD/raft-kotlin_amd/lib/libraft_engine.so
+        for a in d20 def; do
+          A="--steps 20 --warmup 5"; [ $a = def ] && A=""
+          RAFT_ENGINE_LIB=$lib step pmc_${v}_$a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU -d $OUT/pmc_${v}_$a -o run --output-format csv -- python bench.py $A $Q
+        done
+      done
+      for i in 1 2; do
+        for v in prod ${VARIANTS:-}; do
+          lib=$PWD/raft-kotlin_amd/lib/libraft_engine_$v.so; [ $v = prod ] && lib=$PWD/raft-kotlin_amd/lib/libraft_engine.so
+          RAFT_ENGINE_LIB=$lib step t_${v}_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+          RAFT_ENGINE_LIB=$lib step t_${v}_def_$i 200 python -u bench.py $Q
+        done
+      done
+      for f in $OUT/t_*.log; do echo "$(basename $f) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"value": [0-9.e+]*' $f | head -1)"; done > $OUT/timing.txt
+      python scripts/pmc_valu.py $(for v in prod ${VARIANTS:-}; do echo $OUT/pmc_${v}_d20 $OUT/pmc_${v}_def; done) > $OUT/valu.json
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
