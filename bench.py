@@ -594,6 +594,11 @@ def timed_leg(eng, args, chunk, coll, dev, world):
     rows = [counters[q].data_ptr() for q, _ in plan]
     inline = mode == "inline"
     chunk_ev = [torch.cuda.Event() for _ in plan] if inline else []
+    # torch creates an event's HIP event at its first record: done here, so
+    # the records inside the clock are plain hipEventRecord calls (the lazy
+    # creation put ~2 us of host time ahead of the first launch)
+    for e in (ev0, ev1, ar0, ar1, *chunk_ev):
+        e.record(stream)
     torch.cuda.synchronize(dev)
     if coll:
         dist.barrier()
