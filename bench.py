@@ -540,14 +540,17 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
     return out
 
 
-def timed_leg(eng, args, chunk, coll, dev, world):
+def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     """Warmup (untimed), then the timed region of `args.steps` lockstep steps on
     `eng`: enqueued in chunks of `chunk` steps, bracketed by a barrier and a
     device sync on both sides.  When `coll`, the counter rows are all-reduced
     over the ranks: by default (--allreduce end) once, on the engine stream
     after the last launch and before the closing sync, so the collective is
     inside the clock; per chunk in series with the launches (inline); or after
-    the clock stops (after, a diagnostic).  Returns this rank's clock, the
+    the clock stops (after, a diagnostic).  With `comm` (the engine's own RCCL
+    communicator, engine.RaftComm) the in-clock all-reduce is one native call,
+    raft_engine_allreduce_counters, out of place; else torch.distributed's
+    all_reduce after a row copy.  Returns this rank's clock, the
     stream-event, step-kernel and all-reduce times, the job's elapsed time (MAX
     over ranks) and the counter rows (this rank's, all ranks', warmup)."""
     import torch
@@ -572,10 +575,14 @@ def timed_leg(eng, args, chunk, coll, dev, world):
             wev = torch.cuda.Event()
             wev.record(stream)
             comm_stream.wait_event(wev)
-        with torch.cuda.stream(wst):
+        if comm is not None and mode == "end":
             for _ in range(2):
-                wglob.copy_(wcount)
-                dist.all_reduce(wglob)
+                eng.allreduce_counters(comm, wcount.data_ptr(), wglob.data_ptr(), max(1, args.warmup))
+        else:
+            with torch.cuda.stream(wst):
+                for _ in range(2):
+                    wglob.copy_(wcount)
+                    dist.all_reduce(wglob)
     eng.sync()
     torch.cuda.synchronize(dev)
     if coll:
@@ -626,9 +633,12 @@ def timed_leg(eng, args, chunk, coll, dev, world):
         # runs beside the RCCL kernel), before the closing sync.  The copy
         # keeps this rank's own rows for its roofline.
         ar0.record(stream)
-        with torch.cuda.stream(stream):
-            gcounters.copy_(counters)
-            dist.all_reduce(gcounters)
+        if comm is not None:
+            eng.allreduce_counters(comm, rows[0], gcounters.data_ptr(), args.steps)
+        else:
+            with torch.cuda.stream(stream):
+                gcounters.copy_(counters)
+                dist.all_reduce(gcounters)
         ar1.record(stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
@@ -665,7 +675,7 @@ def timed_leg(eng, args, chunk, coll, dev, world):
             "counters": counters, "gcounters": gcounters, "wcount": wcount}
 
 
-def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, scaling, main_rows):
+def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, scaling, main_rows, comm=None):
     """The other scaling's leg of an N > 1 config-3 job, warmed up and timed
     exactly like the main leg (timed_leg).  Rank 0's weak shard holds global
     groups 0..groups-1, which the strong split covers over all ranks, so the
@@ -687,7 +697,7 @@ def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, s
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges
     try:
-        leg = timed_leg(eng, args, chunk, coll, dev, world)
+        leg = timed_leg(eng, args, chunk, coll, dev, world, comm)
     finally:
         eng.close()
     c_all = leg["gcounters"].cpu().numpy()[:, : abi.NUM_COUNTERS]
@@ -807,6 +817,18 @@ def main(argv=None, result=None):
     dev = torch.device("cuda", local)
 
     eng_mod = importlib.import_module("raft-kotlin_amd.engine")
+    # the counter all-reduce's own RCCL communicator (engine.RaftComm): one
+    # native call inside the clock instead of torch's all_reduce (whose host
+    # path is ~150 us, exposed on a short shard, profiles/r5_d); the id goes
+    # to the ranks over the torch process group.  RAFT_BENCH_TORCH_ALLREDUCE=1
+    # keeps torch's all_reduce (and the gloo rehearsal always does: RCCL
+    # refuses two ranks on one GPU)
+    comm = None
+    if coll and backend == "nccl" and os.environ.get("RAFT_BENCH_TORCH_ALLREDUCE") != "1":
+        uid = eng_mod.RaftComm.unique_id() if rank == 0 else bytes(abi.COMM_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+        dist.broadcast(t, 0)
+        comm = eng_mod.RaftComm(bytes(t.cpu().tolist()), world, rank, local)
     kw = dict(abi.CONFIGS[args.config])
     R = kw["R"]
     g0, G_local = shard(args.groups, world, rank, args.scaling)
@@ -840,7 +862,7 @@ def main(argv=None, result=None):
     eng = eng_mod.RaftEngine(params, device=local)
     nsub = eng.subranges                                     # launch sub-ranges of the warmup and timed legs
     hbm_bytes_engine = eng.device_bytes
-    leg = timed_leg(eng, args, chunk, coll, dev, world)
+    leg = timed_leg(eng, args, chunk, coll, dev, world, comm)
     wall, ev_ms, kern_ms, launches = leg["wall"], leg["ev_ms"], leg["kern_ms"], leg["launches"]
     elapsed, kern_avg_ms, kern_avg_per_rank = leg["elapsed"], leg["kern_avg_ms"], leg["kern_avg_per_rank"]
     counters, gcounters, wcount = leg["counters"], leg["gcounters"], leg["wcount"]
@@ -983,7 +1005,7 @@ def main(argv=None, result=None):
         eng = None
         other = "weak" if args.scaling == "strong" else "strong"
         side = side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, other,
-                        (c_all if other == "weak" else c_loc) if rank == 0 else None)
+                        (c_all if other == "weak" else c_loc) if rank == 0 else None, comm)
 
     cfg_name = "config4" if world > 1 and args.config == 3 and args.scaling == "strong" else f"config{args.config}"
     out = {
@@ -1018,7 +1040,10 @@ def main(argv=None, result=None):
             "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window, net) < abi.MAX_STEPS_PER_LAUNCH),
             "counter_allreduce_every": ({"end": "timed_region_once", "inline": chunk,
                                          "after": "after_timed_region_diagnostic"}[args.allreduce] if coll else None),
-            "collective": ({"backend": backend, "ranks": world, "forced_at_one_rank": world == 1} if coll else None),
+            "collective": ({"backend": backend, "ranks": world, "forced_at_one_rank": world == 1,
+                            "counter_allreduce": ("raft_engine_allreduce_counters (the engine's RCCL communicator)"
+                                                  if comm is not None and args.allreduce == "end" else
+                                                  "torch.distributed.all_reduce")} if coll else None),
         },
         "roofline": {
             "bound": "alg_equiv", "basis": "alg_equiv", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1083,6 +1108,8 @@ def main(argv=None, result=None):
                       warmup_counters=wcount.cpu().numpy()[: args.warmup, : abi.NUM_COUNTERS])
     if eng is not None:
         eng.close()
+    if comm is not None:
+        comm.close()
     if coll:
         dist.destroy_process_group()
     return 0

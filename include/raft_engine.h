@@ -317,6 +317,26 @@ int     raft_engine_set_step_index(raft_engine* e, int64_t t);
  * grow-only staging of the handler batches and accessors (kept for the
  * engine's lifetime at 1.25x the largest request; raft_engine_trim_staging
  * frees it, page-locked host staging included). */
+/* ---- multi-GPU: the counter all-reduce ----------------
+ * A sharded run is one engine per GPU, each owning a contiguous range of
+ * global group ids (raft_params.g0); groups never exchange anything, and the
+ * only cross-GPU data is the per-step counter rows, summed over the ranks by
+ * RCCL (over xGMI between MI355X GPUs).  Rank 0 makes an id, the caller
+ * passes it to every rank (any channel), and each rank creates its
+ * communicator (a collective call: it returns once every rank has joined).
+ * raft_engine_allreduce_counters enqueues the sum of n_steps counter rows
+ * [n_steps][RAFT_COUNTER_STRIDE] int64 (device pointers; in place when
+ * out_dev == counters_dev) on the engine's stream, after every step launch
+ * already enqueued there.  RCCL is loaded at the first raft_comm call (never
+ * for one-GPU use); without it these return RAFT_ENODEV. */
+#define RAFT_COMM_ID_BYTES 128
+typedef struct raft_comm raft_comm;
+int raft_comm_get_unique_id(uint8_t id[RAFT_COMM_ID_BYTES]);
+int raft_comm_create(const uint8_t id[RAFT_COMM_ID_BYTES], int32_t nranks, int32_t rank, int device, raft_comm** out);
+int raft_comm_destroy(raft_comm* c);
+int raft_engine_allreduce_counters(raft_engine* e, raft_comm* c, const int64_t* counters_dev, int64_t* out_dev,
+                                   int32_t n_steps);
+
 /* Traffic probe (rocprofv3 calibration; never part of a step): kind 0 moves
  * every chunk's state into registers and back exactly as a step launch's
  * piece entry and exit does (values unchanged); kind 1 makes one 8-byte store

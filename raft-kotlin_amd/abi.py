@@ -24,6 +24,7 @@ RAFT_EDEVICE = -3
 RAFT_ERANGE = -4
 RAFT_ENODEV = -5
 RAFT_EWINDOW = -6
+COMM_ID_BYTES = 128          # include/raft_engine.h RAFT_COMM_ID_BYTES
 
 # enum class State (RaftServer.kt:24-26)
 FOLLOWER, CANDIDATE, LEADER = 0, 1, 2
@@ -285,6 +286,10 @@ def load_library(path: str | None = None):
         "raft_engine_digest_range": (C.c_int, [eng, I64, I64, P(U64)]),
         "raft_engine_check_log_matching": (C.c_int, [eng, I64, I64, P(C.c_uint8), P(I64)]),
         "raft_engine_traffic_probe": (C.c_int, [eng, I32, P(I64), P(I64)]),
+        "raft_comm_get_unique_id": (C.c_int, [P(C.c_uint8)]),
+        "raft_comm_create": (C.c_int, [P(C.c_uint8), I32, I32, C.c_int, P(C.c_void_p)]),
+        "raft_comm_destroy": (C.c_int, [C.c_void_p]),
+        "raft_engine_allreduce_counters": (C.c_int, [eng, C.c_void_p, C.c_void_p, C.c_void_p, I32]),
         "raft_vote_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_vote_req), P(raft_vote_resp), I64]),
         "raft_append_batch": (C.c_int, [eng, P(I64), P(I32), P(raft_append_req), P(raft_append_resp), I64]),
         "raft_append_command_batch": (C.c_int, [eng, P(I64), P(I32), P(C.c_uint32), I64]),
@@ -331,7 +336,8 @@ EXPORTED_SYMBOLS = [
     "raft_engine_set_kernel", "raft_engine_reset", "raft_engine_trim_staging",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
-    "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_engine_traffic_probe", "raft_vote_batch", "raft_append_batch",
+    "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_engine_traffic_probe",
+    "raft_comm_get_unique_id", "raft_comm_create", "raft_comm_destroy", "raft_engine_allreduce_counters", "raft_vote_batch", "raft_append_batch",
     "raft_append_command_batch", "raft_vote_batch_dev", "raft_append_batch_dev", "raft_append_command_batch_dev",
     "raft_philox4x32_10", "raft_host_alloc", "raft_host_free",
     # include/raft_wire.h

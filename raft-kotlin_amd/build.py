@@ -22,13 +22,14 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SRC = os.path.join(CSRC, "raft_engine.hip")
 SRCS = [SRC, os.path.join(CSRC, "raft_wire.cpp"),                   # the wire codec is host code
-        os.path.join(CSRC, "raft_host.cpp")]                         # page-locked batch memory
+        os.path.join(CSRC, "raft_host.cpp"),                         # page-locked batch memory
+        os.path.join(CSRC, "raft_comm.cpp")]                         # the RCCL counter all-reduce (dlopen)
 HDRS = [os.path.join(CSRC, h) for h in ("raft_step.h", "philox.h")] + [
     os.path.join(ROOT, "include", h) for h in ("raft_engine.h", "raft_wire.h")]
 KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h")     # bench.py kernel_source_id
 OUT = os.path.join(PKG, "lib", "libraft_engine.so")
 ARCH = os.environ.get("RAFT_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", "-ldl"]
 
 
 def kernel_source_id() -> str:

@@ -23,6 +23,43 @@ class RaftError(RuntimeError):
     pass
 
 
+class RaftComm:
+    """An RCCL communicator for the counter all-reduce of a sharded run
+    (include/raft_engine.h raft_comm_*): rank 0 makes `unique_id()`, every
+    rank gets it (any channel) and constructs RaftComm(uid, nranks, rank,
+    device); construction returns once every rank has joined."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = abi.load_library()
+        buf = (C.c_uint8 * abi.COMM_ID_BYTES)()
+        if lib.raft_comm_get_unique_id(buf) != abi.RAFT_OK:
+            raise RaftError("raft_comm_get_unique_id: " + lib.raft_last_error().decode(errors="replace"))
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int = 0):
+        self._lib = abi.load_library()
+        if len(uid) != abi.COMM_ID_BYTES:
+            raise ValueError(f"a communicator id is {abi.COMM_ID_BYTES} bytes")
+        buf = (C.c_uint8 * abi.COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        if self._lib.raft_comm_create(buf, nranks, rank, device, C.byref(h)) != abi.RAFT_OK:
+            raise RaftError("raft_comm_create: " + self._lib.raft_last_error().decode(errors="replace"))
+        self._h = h
+        self.nranks, self.rank, self.device = nranks, rank, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.raft_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class RaftEngine:
     def __init__(self, params: abi.raft_params, device: int = 0):
         self._lib = abi.load_library()
@@ -195,6 +232,15 @@ class RaftEngine:
         self._check(self._lib.raft_engine_check_log_matching(self._h, g0, n, abi.ptr(f, C.c_uint8) if flags else None,
                                                              C.byref(out)), "check_log_matching")
         return (int(out.value), f) if flags else int(out.value)
+
+    def allreduce_counters(self, comm: RaftComm, counters_ptr: int, out_ptr: int, n_steps: int):
+        """raft_engine_allreduce_counters: the sum over the ranks of n_steps
+        counter rows (DEVICE pointers, [n_steps][COUNTER_STRIDE] int64; in
+        place when out_ptr == counters_ptr), enqueued on the engine stream
+        after its step launches."""
+        self._check(self._lib.raft_engine_allreduce_counters(self._h, comm._h, C.c_void_p(counters_ptr),
+                                                             C.c_void_p(out_ptr), int(n_steps)),
+                    "raft_engine_allreduce_counters")
 
     def traffic_probe(self, kind: int) -> tuple[int, int]:
         """raft_engine_traffic_probe: one dispatch of the step kernel's own HBM

@@ -42,7 +42,11 @@ def test_forced_collective_at_one_rank(backend, mode, monkeypatch):
     rc = bench.main(argv, result=res)
     assert rc == 0
     out = res["out"]
-    assert out["config"]["collective"] == {"backend": backend, "ranks": 1, "forced_at_one_rank": True}
+    col = out["config"]["collective"]
+    assert (col["backend"], col["ranks"], col["forced_at_one_rank"]) == (backend, 1, True)
+    # the default in-clock all-reduce over RCCL is the engine's own native call
+    native = backend == "nccl" and mode is None
+    assert col["counter_allreduce"].startswith("raft_engine_allreduce_counters") == native
     # the default is the in-clock mode: one all-reduce of the timed rows before the closing sync
     want = {None: "timed_region_once", "inline": 400, "after": "after_timed_region_diagnostic"}[mode]
     assert out["config"]["counter_allreduce_every"] == want
