@@ -83,6 +83,26 @@ case $P in
       for f in $OUT/t_*.log; do echo "$(basename $f) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"value": [0-9.e+]*' $f | head -1)"; done > $OUT/timing.txt
       python scripts/pmc_valu.py $(for v in prod ${VARIANTS:-}; do echo $OUT/pmc_${v}_d20 $OUT/pmc_${v}_def; done) > $OUT/valu.json
       ;;
+  f)  # parity suite (the native RCCL all-reduce included); the in-clock all-reduce through
+      # raft_engine_allreduce_counters vs torch's, full size and 1/8 shard; row 22's bound (log
+      # stores dropped); the default bench's PMC rows
+      step pytest 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+      for i in 1 2; do
+        step d20_plain_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step d20_native_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 RAFT_BENCH_TORCH_ALLREDUCE=1 step d20_torch_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        step s8_plain_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_native_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 RAFT_BENCH_TORCH_ALLREDUCE=1 step s8_torch_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_nostore.so step nostore_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_nostore.so step nostore_def_$i 200 python -u bench.py $Q
+        step prod_def_$i 200 python -u bench.py $Q
+      done
+      for f in $OUT/d20_*.log $OUT/s8_*.log $OUT/nostore_*.log $OUT/prod_*.log; do
+        echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"allreduce_ms": [0-9.enul]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1)"
+      done > $OUT/summary.txt
+      TAG=r5_f_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
