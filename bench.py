@@ -590,7 +590,6 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
 
     # ---- timed region ----
     eng.set_kernel_timing(True)
-    ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ar0 = torch.cuda.Event(enable_timing=True)
     ar1 = torch.cuda.Event(enable_timing=True)
@@ -604,13 +603,14 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     # torch creates an event's HIP event at its first record: done here, so
     # the records inside the clock are plain hipEventRecord calls (the lazy
     # creation put ~2 us of host time ahead of the first launch)
-    for e in (ev0, ev1, ar0, ar1, *chunk_ev):
+    for e in (ev1, ar0, ar1, *chunk_ev):
         e.record(stream)
     torch.cuda.synchronize(dev)
     if coll:
         dist.barrier()
+    # (no marker ahead of the first launch: the stream-event time starts at
+    # that launch's own start timestamp, raft_engine_timed_span)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for ci, (done, k) in enumerate(plan):
         eng.step_async(k, rows[ci])
         if inline:
@@ -653,7 +653,7 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
             dist.all_reduce(gcounters)
             torch.cuda.synchronize(dev)
             after_ms = (time.perf_counter() - t_ar) * 1e3
-    ev_ms = ev0.elapsed_time(ev1)
+    ev_ms = eng.timed_span(ev1.cuda_event)
     allreduce_ms = ar0.elapsed_time(ar1) if mode == "end" else (after_ms if mode == "after" else None)
     kern_ms, launches = eng.kernel_time()
     eng.set_kernel_timing(False)
@@ -1081,8 +1081,8 @@ def main(argv=None, result=None):
                    "allreduce_ms": leg["allreduce_ms"],
                    "note": "the timed region: each rank's wall clock from after the opening barrier + device "
                            "sync to after its closing device sync (the closing barrier follows the clock; the job's "
-                           "time is the MAX over ranks), ms_per_step uses the larger of wall and the stream events "
-                           "around the launches; step_kernel_ms_total is the time during which a step kernel ran "
+                           "time is the MAX over ranks), ms_per_step uses the larger of wall and stream_event_ms (from the "
+                           "first launch's own start timestamp to an event after the last work); step_kernel_ms_total is the time during which a step kernel ran "
                            "(the union of the sub-range launches); the rest is launch latency, the counter "
                            "reductions, the counter all-reduce and the final sync. allreduce_ms: the all-reduce of "
                            "the timed counter rows (with its row copy), stream events around it on the engine "

@@ -294,6 +294,12 @@ void*   raft_engine_stream(raft_engine* e);
  * resets both.  With one sub-range the union is the sum of the launches. */
 int raft_engine_set_kernel_timing(raft_engine* e, int enable);
 int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches);
+/* The time from the start of the first step launch timed since timing was
+ * switched on (the launch's own start timestamp, carried by the dispatch: no
+ * marker ahead of it) to `end_event` (a hipEvent_t the caller recorded after
+ * its last launch); call before raft_engine_kernel_time, which resets the
+ * timed launches. */
+int raft_engine_timed_span(raft_engine* e, void* end_event, double* ms);
 int64_t raft_engine_step_index(raft_engine* e);   /* steps executed so far */
 /* Steps fused into one kernel launch from now on (0 = 1), at most
  * RAFT_MAX_STEPS_PER_LAUNCH.  Results do not depend on it. */

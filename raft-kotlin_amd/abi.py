@@ -267,6 +267,7 @@ def load_library(path: str | None = None):
         "raft_engine_stream": (C.c_void_p, [eng]),
         "raft_engine_set_kernel_timing": (C.c_int, [eng, C.c_int]),
         "raft_engine_kernel_time": (C.c_int, [eng, P(C.c_double), P(I64)]),
+        "raft_engine_timed_span": (C.c_int, [eng, C.c_void_p, P(C.c_double)]),
         "raft_engine_step_index": (I64, [eng]),
         "raft_engine_set_step_index": (C.c_int, [eng, I64]),
         "raft_engine_set_steps_per_launch": (C.c_int, [eng, I32]),
@@ -330,7 +331,7 @@ EXPORTED_SYMBOLS = [
     "raft_params_default", "raft_last_error", "raft_abi_version", "raft_build_source_id",
     "raft_build_kernel_source_id", "raft_engine_create",
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
-    "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time",
+    "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time", "raft_engine_timed_span",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
     "raft_engine_set_subranges", "raft_engine_subranges", "raft_engine_kernel_info", "raft_engine_wait_stream",
     "raft_engine_set_kernel", "raft_engine_reset", "raft_engine_trim_staging",

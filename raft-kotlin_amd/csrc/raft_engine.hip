@@ -1629,6 +1629,23 @@ int raft_engine_kernel_time(raft_engine* e, double* total_ms, int64_t* launches)
     e->timed_launches = 0;
     return check_device_status(e);
 }
+int raft_engine_timed_span(raft_engine* e, void* end_event, double* ms) {
+    if (!e || !end_event || !ms) return fail(RAFT_EINVAL, "null argument");
+    if (e->ev_used < 2) return fail(RAFT_EINVAL, "no timed launch since kernel timing was switched on");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipEventSynchronize((hipEvent_t)end_event));
+    // from the earliest launch start (a sub-range can start a launch ahead of
+    // sub-range 0, see raft_engine_kernel_time) to the caller's event
+    float lo = 0.f, end = 0.f;
+    for (size_t q = 2; q + 1 < e->ev_used; q += 2) {
+        float a = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, e->ev[0], e->ev[q]));
+        lo = std::min(lo, a);
+    }
+    HIP_TRY(hipEventElapsedTime(&end, e->ev[0], (hipEvent_t)end_event));
+    *ms = (double)end - (double)lo;
+    return RAFT_OK;
+}
 int64_t raft_engine_step_index(raft_engine* e) { return e ? (int64_t)e->t : -1; }
 int raft_engine_set_steps_per_launch(raft_engine* e, int32_t k) {
     if (!e) return fail(RAFT_EINVAL, "null engine");

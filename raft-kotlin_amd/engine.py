@@ -242,6 +242,14 @@ class RaftEngine:
                                                              C.c_void_p(out_ptr), int(n_steps)),
                     "raft_engine_allreduce_counters")
 
+    def timed_span(self, end_event_ptr: int) -> float:
+        """raft_engine_timed_span: ms from the first timed step launch's start to
+        the caller's event (e.g. torch.cuda.Event.cuda_event); call before
+        kernel_time()."""
+        ms = C.c_double()
+        self._check(self._lib.raft_engine_timed_span(self._h, C.c_void_p(end_event_ptr), C.byref(ms)), "timed_span")
+        return float(ms.value)
+
     def traffic_probe(self, kind: int) -> tuple[int, int]:
         """raft_engine_traffic_probe: one dispatch of the step kernel's own HBM
         access pattern (kind 0: the state into registers and back; kind 1: one
