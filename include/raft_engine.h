@@ -423,6 +423,16 @@ int raft_append_batch_dev(raft_engine* e, const int64_t* group, const int32_t* d
                           const raft_append_req* req, raft_append_resp* resp, int64_t n);
 int raft_append_command_batch_dev(raft_engine* e, const int64_t* group, const int32_t* replica,
                                   const uint32_t* cmd, int64_t n);
+/* How the batches above order messages (results never depend on it):
+ * RAFT_BATCH_PATH_SORTED, a stable radix sort of every message by
+ * (group, replica); RAFT_BATCH_PATH_BUCKETED, one stable partition into
+ * buckets of 2^S consecutive replicas, each bucket sorted in LDS by the
+ * workgroup that applies it (G * R <= 2^32 only, else RAFT_EINVAL at the
+ * batch); RAFT_BATCH_PATH_AUTO (the default): bucketed where it applies. */
+#define RAFT_BATCH_PATH_AUTO     0
+#define RAFT_BATCH_PATH_SORTED   1
+#define RAFT_BATCH_PATH_BUCKETED 2
+int raft_engine_set_batch_path(raft_engine* e, int32_t path);
 
 /* ---- Philox4x32-10 (shared bit-for-bit with the CPU harness) -----------
  * Counter = (c0 = step, c1 = global group id, c2 = purpose, c3 = sub),

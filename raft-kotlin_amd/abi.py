@@ -125,6 +125,8 @@ class raft_params(C.Structure):
 SCHED_AUTO, SCHED_ONE_PER_WAVE, SCHED_BALANCED = 0, 1, 2
 # step-kernel variant (raft_params.kernel): built for the workload, or the general one
 KERNEL_AUTO, KERNEL_GENERAL = 0, 1
+# raft_engine_set_batch_path
+BATCH_PATH_AUTO, BATCH_PATH_SORTED, BATCH_PATH_BUCKETED = 0, 1, 2
 
 
 class raft_kernel_info(C.Structure):
@@ -276,6 +278,7 @@ def load_library(path: str | None = None):
         "raft_engine_kernel_info": (C.c_int, [eng, P(raft_kernel_info)]),
         "raft_engine_wait_stream": (C.c_int, [eng, C.c_void_p]),
         "raft_engine_set_kernel": (C.c_int, [eng, I32]),
+        "raft_engine_set_batch_path": (C.c_int, [eng, I32]),
         "raft_engine_reset": (C.c_int, [eng]),
         "raft_engine_trim_staging": (C.c_int, [eng]),
         "raft_engine_device_bytes": (I64, [eng]),
@@ -334,7 +337,7 @@ EXPORTED_SYMBOLS = [
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time", "raft_engine_timed_span",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",
     "raft_engine_set_subranges", "raft_engine_subranges", "raft_engine_kernel_info", "raft_engine_wait_stream",
-    "raft_engine_set_kernel", "raft_engine_reset", "raft_engine_trim_staging",
+    "raft_engine_set_kernel", "raft_engine_set_batch_path", "raft_engine_reset", "raft_engine_trim_staging",
     "raft_engine_device_bytes",
     "raft_engine_read_state", "raft_engine_write_state", "raft_engine_read_log",
     "raft_engine_write_log", "raft_engine_digest", "raft_engine_digest_range", "raft_engine_check_log_matching", "raft_engine_traffic_probe",

@@ -8,6 +8,8 @@
 // handlers read or write, and (rarely) non-primary session rows.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
@@ -898,19 +900,14 @@ __global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __rest
     if (!ok) atomicOr(&flags[0], 1u);
 }
 
-// flags[0]: a message was outside the engine (nothing is applied);
+// One replica's run of messages, in batch order: load the replica (idx =
+// g * R + r), apply message ord(m) for m = m0, m0 + 1, ... while more(m), store
+// it back.  Shared by both batch paths (batch_kernel, bucket_batch_kernel).
 // flags[1]: accesses below the retained log window (RAFT_EWINDOW)
-template <bool TB, class Key, int kind>
-__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int n,
-                                                      const Key* __restrict__ keys,
-                                                      const uint32_t* __restrict__ order, const void* req, void* resp,
-                                                      unsigned int* flags) {
-    const int m0 = blockIdx.x * BLOCK + threadIdx.x;
-    if (m0 >= n || *(volatile unsigned int*)&flags[0]) return;
-    const Key key = keys[m0];
-    if (m0 > 0 && keys[m0 - 1] == key) return;                          // not the first of its run
+template <bool TB, int kind, class More, class Ord>
+__device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_t idx, int m0, More more, Ord ord,
+                                          const void* req, void* resp, unsigned int* flags) {
     const int R = p.R;
-    const int64_t idx = (int64_t)key;
     const int64_t i = idx / R;
     const int r = (int)(idx - i * R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
@@ -922,8 +919,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
     derive_cache<VO>(x, lv);
     BatchCounters cnt;
     bool drew = false;
-    for (int m = m0; m < n && keys[m] == key; ++m) {
-        const uint32_t o = order[m];
+    for (int m = m0; more(m); ++m) {
+        const uint32_t o = ord(m);
         if constexpr (kind == BATCH_VOTE) {
             const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
@@ -953,6 +950,200 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
     }
     store_rep<VO>(x, o, drew, p, idx);
     if (cnt.miss) atomicAdd(&flags[1], cnt.miss);
+}
+
+// The sorted path: one thread per sorted position; the first position of each
+// key's run applies the run.  flags[0]: a message was outside the engine
+// (nothing is applied)
+template <bool TB, class Key, int kind>
+__global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, int n,
+                                                      const Key* __restrict__ keys,
+                                                      const uint32_t* __restrict__ order, const void* req, void* resp,
+                                                      unsigned int* flags) {
+    const int m0 = blockIdx.x * BLOCK + threadIdx.x;
+    if (m0 >= n || *(volatile unsigned int*)&flags[0]) return;
+    const Key key = keys[m0];
+    if (m0 > 0 && keys[m0 - 1] == key) return;                          // not the first of its run
+    apply_run<TB, kind>(p, t, (int64_t)key, m0, [&](int m) { return m < n && keys[m] == key; },
+                        [&](int m) { return order[m]; }, req, resp, flags);
+}
+
+// ---- the bucketed path (uint32 keys): a stable partition of each tile instead
+// of a full radix sort.  Bucket b holds the keys [b << S, (b + 1) << S) -- 2^S
+// consecutive replicas, ~BUCKET_MEAN messages of a random batch.  Two kernels:
+//   bucket_tile_kernel:  per tile of TILE messages, its messages stably
+//                        partitioned by bucket inside the tile's own region,
+//                        and the tile's (offset, count) of every bucket, written
+//                        tile-major (coalesced): seg[tile][b]
+//   bucket_batch_kernel: per bucket, the tiles' segments in tile order (a
+//                        block scan of their counts) -- the bucket's messages
+//                        in batch order -- gathered into LDS a chunk of BLOCK
+//                        at a time, sorted stably by key, one thread per run
+// A bucket is applied by one workgroup, chunk after chunk, so a replica's
+// messages keep batch order across chunks too.  Nothing global is scanned or
+// scattered: the only cross-tile step is each bucket's scan of its ntile
+// counts.
+constexpr int TILE_IPT = 16, TILE = BLOCK * TILE_IPT;
+constexpr int BUCKETS_MAX = 3072;                                       // bucket_tile_kernel's LDS: TILE * 8 + 5 * NB * 2 < 64 KB
+constexpr int BUCKET_MEAN = 320;                                        // target messages per bucket
+// bucket_batch_kernel's workgroup: a bucket's chunk, one message per thread
+// (per 10^6-message batch, 512 threads at 320 per bucket beat 256 at 160 and
+// 1,024 at 640 by 5-10 %, profiles/r5_h)
+constexpr int BUCKET_THREADS = 512;
+
+// Wave w of the tile's workgroup takes messages [w * 64 * TILE_IPT, (w + 1) *
+// 64 * TILE_IPT) of it, 64 consecutive ones per round.  A message's place in
+// its bucket's segment: the lanes of its round with its bucket below it (a
+// match by ballots over the bucket bits), plus the wave's earlier rounds (the
+// wave's LDS count, read by every lane of the match and then advanced by its
+// lowest lane), plus the earlier waves (their counts, summed after the tile).
+__global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __restrict__ group,
+                                                            const int32_t* __restrict__ dst, int n, int64_t G, int R,
+                                                            int S, int NB, int bbits, uint2* __restrict__ tiles,
+                                                            uint2* __restrict__ seg, unsigned int* flags) {
+    // LDS: the tile's output staged (written out coalesced: one 8-B store per
+    // message to its place would cost a 32-B sector each), then the waves'
+    // counts and the tile's bucket offsets, [WAVES_PER_BLOCK + 1][NB] (<= TILE)
+    extern __shared__ uint2 stage[];                                    // [TILE]
+    uint16_t* const cnt = (uint16_t*)(stage + TILE);
+    for (int b = threadIdx.x; b < WAVES_PER_BLOCK * NB; b += BLOCK) cnt[b] = 0;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint16_t* const cw = cnt + w * NB;
+    uint16_t* const off = cnt + WAVES_PER_BLOCK * NB;                    // the tile's bucket offsets
+    const uint64_t below = (1ull << lane) - 1ull;
+    const int t0 = blockIdx.x * TILE;
+    const int base = t0 + w * 64 * TILE_IPT + lane;
+    // every round's message loaded up front (the rounds' ballots and LDS
+    // updates would otherwise serialise the loads)
+    // (unconditional loads at a clamped index: a load under a branch is
+    // waited for inside it, which serialised the 2 * TILE_IPT round trips)
+    uint32_t key[TILE_IPT], rk[TILE_IPT];
+    int64_t gg[TILE_IPT];
+    int32_t dd[TILE_IPT];
+#pragma unroll
+    for (int j = 0; j < TILE_IPT; ++j) {
+        const int m = min(base + j * 64, n - 1);
+        gg[j] = group[m];
+        dd[j] = dst[m];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < TILE_IPT; ++j) {
+        const bool in = base + j * 64 < n;
+        const bool ok = gg[j] >= 0 && gg[j] < G && dd[j] >= 0 && dd[j] < R;
+        key[j] = in && ok ? (uint32_t)((uint64_t)gg[j] * (uint64_t)R + (uint64_t)dd[j]) : 0u;
+        bad |= in && !ok;
+    }
+    if (bad) atomicOr(&flags[0], 1u);
+    __syncthreads();                                                    // the counts are zero
+#pragma unroll
+    for (int j = 0; j < TILE_IPT; ++j) {
+        const bool in = base + j * 64 < n;
+        const uint32_t b = key[j] >> S;
+        uint64_t peers = __ballot(in);
+        for (int i = 0; i < bbits; ++i) {
+            const uint64_t x = __ballot((b >> i) & 1u);
+            peers &= ((b >> i) & 1u) ? x : ~x;
+        }
+        uint32_t old = 0;
+        if (in) {
+            old = cw[b];                                                // every lane of the match reads it,
+            if (lane == __builtin_ctzll(peers)) cw[b] = (uint16_t)(old + (uint32_t)__popcll(peers));   // then its first lane
+        }
+        rk[j] = old + (uint32_t)__popcll(peers & below);
+    }
+    __syncthreads();
+    // the waves' counts -> their prefixes; the tile's count per bucket, and
+    // its exclusive scan over the buckets (each thread a contiguous range of
+    // buckets, then a block scan of the ranges' sums)
+    const int per = (NB + BLOCK - 1) / BLOCK, b0 = threadIdx.x * per, b1 = min(NB, b0 + per);
+    uint32_t sum = 0;
+    for (int b = b0; b < b1; ++b) {
+        uint32_t c = 0;
+        for (int q = 0; q < WAVES_PER_BLOCK; ++q) {
+            const uint32_t x = cnt[q * NB + b];
+            cnt[q * NB + b] = (uint16_t)c;
+            c += x;
+        }
+        off[b] = (uint16_t)c;                                           // (the count, for now)
+        sum += c;
+    }
+    uint32_t pre;
+    rocprim::block_scan<uint32_t, BLOCK>().exclusive_scan(sum, pre, 0u);
+    for (int b = b0; b < b1; ++b) {
+        const uint32_t c = off[b];
+        off[b] = (uint16_t)pre;
+        seg[(int64_t)blockIdx.x * NB + b] = make_uint2(pre, c);
+        pre += c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TILE_IPT; ++j) {
+        const int m = base + j * 64;
+        if (m < n) {
+            const uint32_t b = key[j] >> S;
+            stage[off[b] + cw[b] + rk[j]] = make_uint2(key[j], (uint32_t)m);   // (key, message index)
+        }
+    }
+    __syncthreads();
+    const int len = min(TILE, n - t0);
+    for (int q = threadIdx.x; 2 * q < len; q += BLOCK) {                 // two messages per 16-B store
+        if (2 * q + 1 < len) *(uint4*)&tiles[t0 + 2 * q] = *(const uint4*)&stage[2 * q];
+        else tiles[t0 + 2 * q] = stage[2 * q];
+    }
+}
+
+template <bool TB, int kind, int NT>
+__global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t t, int n, int S, int NB, int ntile,
+                                                          const uint2* __restrict__ tiles,
+                                                          const uint2* __restrict__ seg, const void* req,
+                                                          void* resp, unsigned int* flags) {
+    using Sort = rocprim::block_radix_sort<uint32_t, NT, 1, uint32_t>;
+    using Scan = rocprim::block_scan<uint32_t, NT>;
+    __shared__ union {
+        typename Sort::storage_type sort;
+        typename Scan::storage_type scan;
+    } sm;
+    __shared__ uint2 buf[NT];
+    __shared__ uint32_t lk[NT], lo[NT];
+    if (*(volatile unsigned int*)&flags[0]) return;                   // the same for the whole grid
+    const int bk = blockIdx.x;
+    const uint32_t kb = (uint32_t)bk << S;
+    // this thread's tiles [tt0, tt1): their segments of this bucket, and
+    // where they start in the bucket's batch order
+    const int per = (ntile + NT - 1) / NT, tt0 = threadIdx.x * per, tt1 = min(ntile, tt0 + per);
+    uint32_t mine = 0;
+    for (int q = tt0; q < tt1; ++q) mine += seg[(int64_t)q * NB + bk].y;
+    uint32_t pos, len_all;
+    Scan().exclusive_scan(mine, pos, 0u, len_all, sm.scan, rocprim::plus<uint32_t>());
+    for (uint32_t c0 = 0; c0 < len_all; c0 += NT) {                  // workgroup-uniform
+        const int len = (int)min(len_all - c0, (uint32_t)NT);
+        // the chunk's messages [c0, c0 + len) of the bucket into buf, in batch order
+        uint32_t at = pos;
+        for (int q = tt0; q < tt1 && at < c0 + len; ++q) {
+            const uint2 sg = seg[(int64_t)q * NB + bk];
+            const uint32_t lo_i = max(at, c0), hi_i = min(at + sg.y, c0 + (uint32_t)len);
+            for (uint32_t i = lo_i; i < hi_i; ++i) buf[i - c0] = tiles[(int64_t)q * TILE + sg.x + (i - at)];
+            at += sg.y;
+        }
+        __syncthreads();                                                // buf complete (and sm.scan / sm.sort free)
+        const int q = threadIdx.x;
+        const uint2 x = q < len ? buf[q] : make_uint2(kb + (1u << S), 0u);   // padding sorts last
+        uint32_t k[1] = {x.x - kb}, v[1] = {x.y};
+        Sort().sort(k, v, sm.sort, 0, S + 1);
+        lk[q] = k[0];
+        lo[q] = v[0];
+        __syncthreads();
+        if (q < len && (q == 0 || lk[q - 1] != lk[q])) {
+            const uint32_t key = lk[q];
+            apply_run<TB, kind>(p, t, (int64_t)(kb + key), q, [&](int m) { return m < len && lk[m] == key; },
+                                [&](int m) { return lo[m]; }, req, resp, flags);
+        }
+        // another chunk of this bucket: the barrier (a workgroup-scope fence:
+        // one CU, one L1) makes this chunk's replica stores visible to it, and
+        // frees buf / lk / lo
+        if (c0 + NT < len_all) __syncthreads();
+    }
 }
 
 // read_log / write_log: the host's [n][R][log_cap] image of groups [g0, g0+n)
@@ -1024,6 +1215,7 @@ struct raft_engine {
     char* hst;
     size_t hst_bytes;
     unsigned int* bflags_host;
+    int batch_path;             // RAFT_BATCH_PATH_* (raft_engine_set_batch_path)
     char* aux;                  // device staging of the state / log / digest accessors, grow-only
     size_t aux_bytes;
     int64_t* counters_dev;      // [K][STRIDE] scratch
@@ -1674,6 +1866,13 @@ int raft_engine_wait_stream(raft_engine* e, void* stream) {
     e->fork_needed = true;                 // the sub-range streams must see it too
     return RAFT_OK;
 }
+int raft_engine_set_batch_path(raft_engine* e, int32_t path) {
+    if (!e) return fail(RAFT_EINVAL, "null engine");
+    if (path < RAFT_BATCH_PATH_AUTO || path > RAFT_BATCH_PATH_BUCKETED) return fail(RAFT_EINVAL, "unknown batch path");
+    e->batch_path = path;
+    return RAFT_OK;
+}
+
 int raft_engine_set_kernel(raft_engine* e, int32_t kernel) {
     if (!e) return fail(RAFT_EINVAL, "null engine");
     if (kernel != RAFT_KERNEL_AUTO && kernel != RAFT_KERNEL_GENERAL)
@@ -1973,8 +2172,47 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
     return RAFT_OK;
 }
 
-// The batch on device buffers: keys, a stable radix sort over the key bits,
-// the handlers; one synchronisation at the end for the status flags.
+using BK = void (*)(DevParams, uint32_t, int, int, int, int, const uint2*, const uint2*, const void*, void*,
+                    unsigned int*);
+static BK bucket_kernel_of(int kind, bool tb) {
+    constexpr int NT = BUCKET_THREADS;
+    return kind == BATCH_VOTE     ? (tb ? bucket_batch_kernel<true, BATCH_VOTE, NT> : bucket_batch_kernel<false, BATCH_VOTE, NT>)
+           : kind == BATCH_APPEND ? (tb ? bucket_batch_kernel<true, BATCH_APPEND, NT> : bucket_batch_kernel<false, BATCH_APPEND, NT>)
+                                  : (tb ? bucket_batch_kernel<true, BATCH_COMMAND, NT> : bucket_batch_kernel<false, BATCH_COMMAND, NT>);
+}
+
+// The bucketed path (bucket_tile_kernel, bucket_batch_kernel): buckets of 2^S
+// keys, S the smallest shift that gives ~BUCKET_MEAN messages per bucket of a
+// uniform batch and at most BUCKETS_MAX buckets.
+static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
+                             void* resp, int n, uint64_t nkeys) {
+    int S = 0;
+    while (S < 31 && ((uint64_t)n << S) < (uint64_t)BUCKET_MEAN * nkeys) ++S;
+    while (S < 31 && ((nkeys + (1ull << S) - 1) >> S) > (uint64_t)BUCKETS_MAX) ++S;
+    const int NB = (int)((nkeys + (1ull << S) - 1) >> S);
+    int bbits = 1;
+    while ((uint64_t)(NB - 1) >> bbits) ++bbits;
+    const int ntile = (n + TILE - 1) / TILE;
+    const size_t b_t = al256((size_t)ntile * TILE * 8), b_s = al256((size_t)NB * ntile * 8);
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, b_t + b_s + 256)) return rc;
+    char* b = e->bst;
+    uint2* tiles = (uint2*)b; b += b_t;
+    uint2* seg = (uint2*)b; b += b_s;
+    unsigned int* flags = (unsigned int*)b;
+    HIP_TRY(hipMemsetAsync(flags, 0, 8, e->stream));
+    bucket_tile_kernel<<<ntile, BLOCK, (size_t)TILE * 8 + (size_t)(WAVES_PER_BLOCK + 1) * NB * 2, e->stream>>>(
+        group, dst, n, e->p.G, e->p.R, S, NB, bbits, tiles, seg, flags);
+    const BK kern = bucket_kernel_of(kind, e->p.mode == RAFT_MODE_TEXTBOOK);
+    kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, flags);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return RAFT_OK;
+}
+
+// The batch on device buffers: keys, the bucketed partition or a stable radix
+// sort over the key bits, the handlers; one synchronisation at the end for the
+// status flags.
 static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
                          void* resp, int64_t n64) {
     e->fork_needed = true;
@@ -1982,8 +2220,12 @@ static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const i
     const uint64_t nkeys = (uint64_t)e->p.G * (uint64_t)e->p.R;
     int bits = 1;
     while (bits < 64 && (nkeys - 1) >> bits) ++bits;
-    const int rc = bits <= 32 ? run_batch_keys<uint32_t>(e, kind, group, dst, req, resp, n, bits)
-                              : run_batch_keys<uint64_t>(e, kind, group, dst, req, resp, n, bits);
+    if (e->batch_path == RAFT_BATCH_PATH_BUCKETED && bits > 32)
+        return fail(RAFT_EINVAL, "the bucketed batch path needs G * R <= 2^32");
+    const int rc = e->batch_path != RAFT_BATCH_PATH_SORTED && bits <= 32
+                       ? run_batch_buckets(e, kind, group, dst, req, resp, n, nkeys)
+                   : bits <= 32 ? run_batch_keys<uint32_t>(e, kind, group, dst, req, resp, n, bits)
+                                : run_batch_keys<uint64_t>(e, kind, group, dst, req, resp, n, bits);
     if (rc) return rc;
     e->cache_valid = false;
     if (e->bflags_host[0]) return fail(RAFT_ERANGE, "a message's group or replica index is outside the engine; "

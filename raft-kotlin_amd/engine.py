@@ -133,6 +133,11 @@ class RaftEngine:
         results do not depend on it)."""
         self._check(self._lib.raft_engine_set_kernel(self._h, int(kernel)), "set_kernel")
 
+    def set_batch_path(self, path: int):
+        """How the handler batches order their messages (abi.BATCH_PATH_AUTO /
+        _SORTED / _BUCKETED; results do not depend on it)."""
+        self._check(self._lib.raft_engine_set_batch_path(self._h, int(path)), "set_batch_path")
+
     def reset(self):
         """Every group back to its initial state at step 0 (as created)."""
         self._check(self._lib.raft_engine_reset(self._h), "reset")

@@ -20,12 +20,14 @@ RaftEngine = importlib.import_module("raft-kotlin_amd.engine").RaftEngine
 N = int(os.environ.get("HANDLER_N", "1000000"))
 REPS = int(os.environ.get("HANDLER_REPS", "5"))
 G = int(os.environ.get("HANDLER_G", "1000000"))
+PATH = int(os.environ.get("HANDLER_PATH", "0"))        # abi.BATCH_PATH_*: 0 auto, 1 sorted, 2 bucketed
 
 
 def main():
     kw = dict(abi.CONFIGS[3], G=G)
     R = kw["R"]
     e = RaftEngine(abi.make_params(log_cap=300, steps_per_launch=200, **kw))
+    e.set_batch_path(PATH)
     e.step(200, counters=False)
     st = e.read_state()
     max_term = int(st[:, [r * abi.NUM_FIELDS + abi.F_INDEX["term"] for r in range(R)]].max())
@@ -43,7 +45,7 @@ def main():
             fn(d_group.data_ptr(), d_dst.data_ptr(), d_req.data_ptr(), d_resp.data_ptr(), N)
         plan.append([kind, REPS])
     e.close()
-    print(json.dumps({"n": N, "groups": G, "replicas": R, "kernel_src": bench.kernel_source_id(), "plan": plan}))
+    print(json.dumps({"n": N, "batch_path": PATH, "groups": G, "replicas": R, "kernel_src": bench.kernel_source_id(), "plan": plan}))
 
 
 if __name__ == "__main__":

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 P=${PRESET:?set PRESET}
-OUT=gpurun_out/r5_$P; mkdir -p "$OUT"
+OUT=gpurun_out/r5_$P${TAGS:-}; mkdir -p "$OUT"
 step() {   # step NAME LIMIT CMD...
   local name=$1 lim=$2; shift 2
   timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
@@ -102,6 +102,41 @@ case $P in
         echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"allreduce_ms": [0-9.enul]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1)"
       done > $OUT/summary.txt
       TAG=r5_f_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
+      ;;
+  g)  # the round's evidence at the working tree's kernel: parity suite, smoke, the driver's and the
+      # default bench lines, the 1/8 shard's timeline with the native in-clock all-reduce, PMC rows
+      step pytest 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      step bench_default 600 python -u bench.py
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step trace_s8_native 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $OUT/trace_s8_native -o run --output-format csv -- python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      python scripts/trace_timeline.py $OUT/trace_s8_native > $OUT/timeline_s8_native.json
+      rm -rf $OUT/trace_s8_native
+      TAG=r5_g_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
+      TAG=r5_g_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
+      ;;
+  h)  # the bucketed handler-batch path: its parity tests, then a kernel trace of 5 vote + 5
+      # append batches of 10^6 messages on each path, and the bench's handler leg
+      step pytest 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -k "handler or batch" --timeout 300 --timeout-method thread
+      for path in 1 2; do
+        HANDLER_PATH=$path step htrace_p$path 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_p$path -o run --output-format csv -- python -u scripts/handler_probe.py
+      done
+      step bench_handler 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0
+      ;;
+  h2)  # the bucketed handler path: its parity tests, a kernel trace of both paths, the bench's handler leg
+      step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "handler or batch" --timeout 300 --timeout-method thread
+      for mt in ${SWEEP:-}; do      # m:t = RAFT_BUCKET_MEAN:RAFT_BUCKET_THREADS (experiment switches)
+        m=${mt%:*}; t=${mt#*:}
+        RAFT_BUCKET_THREADS=$t step pytest_$t 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "handler or batch" --timeout 300 --timeout-method thread
+        RAFT_BUCKET_MEAN=$m RAFT_BUCKET_THREADS=$t HANDLER_REPS=3 step htrace_${m}_$t 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_${m}_$t -o run --output-format csv -- python -u scripts/handler_probe.py
+      done
+      HANDLER_REPS=3 step htrace_bucketed 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_bucketed -o run --output-format csv -- python -u scripts/handler_probe.py
+      if [ -n "${HPMC:-}" ]; then   # the bucketed kernels' counters (one pass per counter group)
+        HANDLER_REPS=1 step hpmc_sq 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAIT_ANY --kernel-include-regex "bucket|batch_kernel" -d $OUT/hpmc_sq -o run --output-format csv -- python -u scripts/handler_probe.py
+        HANDLER_REPS=1 step hpmc_fetch 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "bucket|batch_kernel" -d $OUT/hpmc_fetch -o run --output-format csv -- python -u scripts/handler_probe.py
+      fi
+      HANDLER_PATH=1 HANDLER_REPS=3 step htrace_sorted 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_sorted -o run --output-format csv -- python -u scripts/handler_probe.py
+      step bench_handler 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0
       ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh

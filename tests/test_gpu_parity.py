@@ -739,31 +739,101 @@ def test_handler_batches_vs_oracle(R, mode, G, n, window):
         w, lt, lc = random_ring_states(rng, G, R, cap, window)
     else:
         w, lt, lc = random_states(rng, G, R, cap)
-    e, o = pair(R=R, G=G, log_cap=cap, log_window=window, seed=3, mode=mode)
-    for x in (e, o):
+    grp, dst, vq, aq, cmd = handler_messages(rng, n, G, R, cap, w, window)
+    se = check_handler_batches(R, G, cap, window, mode, w, lt, lc, grp, dst, vq, aq, cmd)
+    if window:
+        # the rows wrapped: some replica holds more physical slots than the ring
+        assert int(np.max(se[:, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(R)]])) > window
+
+
+def check_handler_batches(R, G, cap, window, mode, w, lt, lc, grp, dst, vq, aq, cmd):
+    """A vote, an append and a command batch of the same (group, dst) on two
+    engines -- the bucketed batch path (the default) and the sorted one --
+    against the oracle's handlers applied message by message in batch order;
+    returns the bucketed engine's final state."""
+    o = O.Oracle(abi.make_params(R=R, G=G, log_cap=cap, log_window=window, seed=3, mode=mode))
+    engines = []
+    for path in (abi.BATCH_PATH_BUCKETED, abi.BATCH_PATH_SORTED):
+        e = RaftEngine(abi.make_params(R=R, G=G, log_cap=cap, log_window=window, seed=3, mode=mode))
+        e.set_batch_path(path)
+        engines.append(e)
+    for x in (*engines, o):
         x.write_state(w)
         x.write_log(lt, lc)
-    grp, dst, vq, aq, cmd = handler_messages(rng, n, G, R, cap, w, window)
-    ve = e.vote_batch(grp, dst, vq)
     vo = np.array([o.vote(int(g), int(d), *map(int, q)) for g, d, q in zip(grp, dst, vq)], dtype=np.int32)
-    assert np.array_equal(ve, vo), f"vote responses differ at {np.argwhere(np.any(ve != vo, axis=1))[:3].ravel()}"
-    ae = e.append_batch(grp, dst, aq)
     ao = []
     for g, d, q in zip(grp, dst, aq):
         t, s, st = o.append(int(g), int(d), int(q[0]), int(q[1]), int(q[2]), int(q[3]),
                             (int(q[5]), int(q[6])) if q[4] else None, int(q[7]))
         ao.append((t, int(s), st))
     ao = np.array(ao, dtype=np.int32)
-    assert np.array_equal(ae, ao), f"append responses differ at {np.argwhere(np.any(ae != ao, axis=1))[:3].ravel()}"
-    e.append_command_batch(grp, dst, cmd)
     for g, d, c in zip(grp, dst, cmd):
         o.append_command(int(g), int(d), int(c))
-    se = e.read_state()
-    assert_same_state(se, o.read_state(), R, "handlers")
-    assert_same_logs(se, e.read_log(), o.read_log(), R, "handlers")
-    if window:
-        # the rows wrapped: some replica holds more physical slots than the ring
-        assert int(np.max(se[:, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(R)]])) > window
+    so = o.read_state()
+    for e, name in zip(engines, ("bucketed", "sorted")):
+        ve = e.vote_batch(grp, dst, vq)
+        assert np.array_equal(ve, vo), f"{name}: vote responses differ at {np.argwhere(np.any(ve != vo, axis=1))[:3].ravel()}"
+        ae = e.append_batch(grp, dst, aq)
+        assert np.array_equal(ae, ao), f"{name}: append responses differ at {np.argwhere(np.any(ae != ao, axis=1))[:3].ravel()}"
+        e.append_command_batch(grp, dst, cmd)
+        se = e.read_state()
+        assert_same_state(se, so, R, f"{name} handlers")
+        assert_same_logs(se, e.read_log(), o.read_log(), R, f"{name} handlers")
+    return engines[0].read_state()
+
+
+def test_handler_batches_skewed_vs_oracle():
+    """Half of the messages to one replica (a run of ~3000 across many of the
+    bucketed path's 256-message chunks, and a bucket far above the mean), the
+    rest random: both batch paths against the oracle."""
+    rng = np.random.default_rng(29)
+    R, G, cap, n = 5, 300, 8, 6000
+    w, lt, lc = random_states(rng, G, R, cap)
+    grp, dst, vq, aq, cmd = handler_messages(rng, n, G, R, cap)
+    hot = rng.random(n) < 0.5
+    grp = np.where(hot, 7, grp)
+    dst = np.where(hot, 2, dst).astype(np.int32)
+    check_handler_batches(R, G, cap, 0, abi.MODE_REFERENCE, w, lt, lc, grp, dst, vq, aq, cmd)
+
+
+def test_batch_paths_agree_at_scale():
+    """4.2·10^6 votes over 10^6 groups of 5 (the bucketed path's bucket-count
+    cap applies: S is raised until at most 16384 buckets remain), then 10^6
+    appends: the bucketed and the sorted path leave the same responses, state
+    and logs."""
+    import torch
+    rng = np.random.default_rng(31)
+    R, G, cap = 5, 1_000_000, 8
+    dev = torch.device("cuda:0")
+    engines = []
+    for path in (abi.BATCH_PATH_BUCKETED, abi.BATCH_PATH_SORTED):
+        e = RaftEngine(abi.make_params(R=R, G=G, log_cap=cap, seed=9))
+        e.set_batch_path(path)
+        e.step(3)
+        engines.append(e)
+    outs = []
+    for kind, n in (("vote", 4_200_000), ("append", 1_000_000)):
+        grp = torch.from_numpy(rng.integers(0, G, n)).to(dev)
+        dst = torch.from_numpy(rng.integers(0, R, n).astype(np.int32)).to(dev)
+        if kind == "vote":
+            req = torch.from_numpy(np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(0, cap + 1, n),
+                                             rng.integers(0, 4, n)], axis=1).astype(np.int32)).to(dev)
+        else:
+            req = torch.from_numpy(np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), rng.integers(-1, cap, n),
+                                             rng.integers(-1, 4, n), rng.integers(0, 2, n), rng.integers(0, 6, n),
+                                             rng.integers(0, 1 << 32, n, dtype=np.uint64), rng.integers(0, 8, n)],
+                                            axis=1).astype(np.int64).astype(np.uint32).view(np.int32)).to(dev)
+        torch.cuda.synchronize(dev)                  # the engine stream does not wait for torch's
+        res = []
+        for e in engines:
+            resp = torch.zeros((n, 2 if kind == "vote" else 3), dtype=torch.int32, device=dev)
+            fn = e.vote_batch_dev if kind == "vote" else e.append_batch_dev
+            fn(grp.data_ptr(), dst.data_ptr(), req.data_ptr(), resp.data_ptr(), n)
+            res.append(resp.cpu().numpy())
+        assert np.array_equal(res[0], res[1]), f"{kind} responses differ"
+    a, b = (e.read_state() for e in engines)
+    assert np.array_equal(a, b)
+    assert engines[0].digest() == engines[1].digest()
 
 
 def test_pinned_host_batches_match_pageable():
