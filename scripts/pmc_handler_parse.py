@@ -1,6 +1,7 @@
 """Parse scripts/pmc_handler.sh output: per handler batch (a batch_keys_kernel
-dispatch starts one) the HBM bytes of all its kernels (keys, the hipcub radix
-sort, batch_kernel) and of batch_kernel alone, from FETCH_SIZE / WRITE_SIZE
+or bucket_tile_kernel dispatch starts one) the HBM bytes of all its kernels
+(bucketed path: the tile partition and bucket_batch_kernel; sorted path: keys,
+the rocprim radix sort, batch_kernel) and of the handler kernel alone, from FETCH_SIZE / WRITE_SIZE
 with the calibration engine's counter-to-bytes factors (scripts/pmc_parse.py),
 and the kernels' durations from the trace.  Rows (one per batch kind) ->
 <dir>/handler_rows.json; `--merge` folds them into profiles/pmc_handler.json,
@@ -58,10 +59,12 @@ def runs(names):
 
 
 def batches(rows):
-    """Group a dispatch list into handler batches: each starts at a batch_keys_kernel."""
+    """Group a dispatch list into handler batches: each starts at its first
+    kernel (batch_keys_kernel on the sorted path, bucket_tile_kernel on the
+    bucketed one)."""
     out, cur = [], None
     for _, n, v in rows:
-        if "batch_keys_kernel" in n:
+        if "batch_keys_kernel" in n or "bucket_tile_kernel" in n:
             cur = []
             out.append(cur)
         if cur is not None:
@@ -92,7 +95,8 @@ def main(d):
         hfetch, hwrite = avg(fb, hk) * 1024 * ff, avg(wb, hk) * 1024 * wf
         t_all, t_h = avg(tb) / 1e6, avg(tb, hk) / 1e6
         rows.append({"kind": kind, "n": n, "groups": plan["groups"], "replicas": plan["replicas"],
-                     "kernel_src": plan["kernel_src"], "batches_averaged": len(ix),
+                     "kernel_src": plan["kernel_src"], "batch_path": plan.get("batch_path", 0),
+                     "batches_averaged": len(ix),
                      "hbm_bytes_per_batch": fetch + write, "hbm_bytes_per_message": (fetch + write) / n,
                      "handler_kernel_hbm_bytes_per_message": (hfetch + hwrite) / n,
                      "handler_kernel_fetch_bytes": hfetch, "handler_kernel_write_bytes": hwrite,

@@ -104,7 +104,7 @@ case $P in
       TAG=r5_f_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
       ;;
   g)  # the round's evidence at the working tree's kernel: parity suite, smoke, the driver's and the
-      # default bench lines, the 1/8 shard's timeline with the native in-clock all-reduce, PMC rows
+      # default bench lines, the 1/8 shard's timeline with the native in-clock all-reduce
       step pytest 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
       step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
       step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
@@ -112,8 +112,6 @@ case $P in
       RAFT_BENCH_FORCE_COLLECTIVE=1 step trace_s8_native 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $OUT/trace_s8_native -o run --output-format csv -- python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
       python scripts/trace_timeline.py $OUT/trace_s8_native > $OUT/timeline_s8_native.json
       rm -rf $OUT/trace_s8_native
-      TAG=r5_g_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
-      TAG=r5_g_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
       ;;
   h)  # the bucketed handler-batch path: its parity tests, then a kernel trace of 5 vote + 5
       # append batches of 10^6 messages on each path, and the bench's handler leg
@@ -141,6 +139,7 @@ case $P in
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
+      TAG=r5_${TAGP:-pmc} step pmc_handler 600 bash scripts/pmc_handler.sh
       ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
