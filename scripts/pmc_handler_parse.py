@@ -18,6 +18,10 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 import pmc_parse  # noqa: E402
 
 OUT_FILE = os.path.join(ROOT, "profiles", "pmc_handler.json")
+# the calibration engine of scripts/traffic_run.py calib: every launch moves
+# exactly CALIB_G * (CALIB_R * REPLICA_BYTES + GROUP_BYTES) bytes each way
+CALIB_G, CALIB_R = int(os.environ.get("TRAFFIC_GROUPS", "1000000")), 5
+REPLICA_BYTES, GROUP_BYTES = 4 * 13 + 8, 12
 
 
 def kernels(d, counter=None):
@@ -74,7 +78,7 @@ def batches(rows):
 
 def main(d):
     plan = json.loads([ln for ln in open(f"{d}/trace.log") if ln.startswith("{")][-1])
-    state = pmc_parse.CALIB_G * (pmc_parse.CALIB_R * pmc_parse.REPLICA_BYTES + pmc_parse.GROUP_BYTES)
+    state = CALIB_G * (CALIB_R * REPLICA_BYTES + GROUP_BYTES)
     cf = sorted(pmc_parse.dispatches(f"{d}/calib_FETCH_SIZE").get("FETCH_SIZE", []))
     cw = sorted(pmc_parse.dispatches(f"{d}/calib_WRITE_SIZE").get("WRITE_SIZE", []))
     ff, wf = state / (cf[len(cf) // 2] * 1024.0), state / (cw[len(cw) // 2] * 1024.0)
