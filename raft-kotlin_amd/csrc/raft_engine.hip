@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "raft_step.h"
@@ -907,11 +908,17 @@ __global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __rest
 template <bool TB, int kind, class More, class Ord>
 __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_t idx, int m0, More more, Ord ord,
                                           const void* req, void* resp, unsigned int* flags) {
+    using Req = std::conditional_t<kind == BATCH_VOTE, raft_vote_req,
+                                   std::conditional_t<kind == BATCH_APPEND, raft_append_req, uint32_t>>;
     const int R = p.R;
     const int64_t i = idx / R;
     const int r = (int)(idx - i * R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
     constexpr bool VO = kind == BATCH_VOTE;
+    // the run's first request is fetched with the replica's fields (one round
+    // trip for both); each later one while the previous message is applied
+    uint32_t om = ord(m0);
+    Req q = ((const Req*)req)[om];
     RepState x;
     load_rep<VO>(x, p, idx);
     const RepState o = x;
@@ -919,34 +926,38 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
     derive_cache<VO>(x, lv);
     BatchCounters cnt;
     bool drew = false;
-    for (int m = m0; more(m); ++m) {
-        const uint32_t o = ord(m);
+    for (int m = m0;;) {
+        const Req qm = q;
+        const uint32_t oc = om;
+        if (more(m + 1)) {
+            om = ord(m + 1);
+            q = ((const Req*)req)[om];
+        }
         if constexpr (kind == BATCH_VOTE) {
-            const raft_vote_req q = ((const raft_vote_req*)req)[o];
             int32_t rt;
             uint64_t gr;
-            vote_handler<TB, true>(x.ref(), __ballot(1), r + 1, q.term, q.candidate_id, q.last_log_index, q.last_log_term,
-                                   __ballot(x.phys - x.last >= p.W), __ballot(x.last >= 1), follower_sent(x.fl), cnt,
-                                   rt, gr);
-            ((raft_vote_resp*)resp)[o] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
+            vote_handler<TB, true>(x.ref(), __ballot(1), r + 1, qm.term, qm.candidate_id, qm.last_log_index,
+                                   qm.last_log_term, __ballot(x.phys - x.last >= p.W), __ballot(x.last >= 1),
+                                   follower_sent(x.fl), cnt, rt, gr);
+            ((raft_vote_resp*)resp)[oc] = raft_vote_resp{rt, ib(gr) ? 1 : 0};
         } else if constexpr (kind == BATCH_APPEND) {
-            const raft_append_req q = ((const raft_append_req*)req)[o];
             int32_t rt = 0;
             uint64_t su = 0, st = 0;
-            const int32_t pv = q.prev_log_index;
+            const int32_t pv = qm.prev_log_index;
             const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
             const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
-            const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, q.term, q.leader_id, pv,
-                                                       q.prev_log_term, __ballot(q.has_entry != 0),
-                                                       Entry{q.entry_term, q.entry_cmd}, q.leader_commit, dprev, dnext,
-                                                       __ballot(pv + 1 == x.last), __ballot(pv >= 0),
-                                                       __ballot(q.leader_id != r + 1), follower_sent(x.fl),
+            const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, qm.term, qm.leader_id,
+                                                       pv, qm.prev_log_term, __ballot(qm.has_entry != 0),
+                                                       Entry{qm.entry_term, qm.entry_cmd}, qm.leader_commit, dprev,
+                                                       dnext, __ballot(pv + 1 == x.last), __ballot(pv >= 0),
+                                                       __ballot(qm.leader_id != r + 1), follower_sent(x.fl),
                                                        cnt, rt, su, st);
-            ((raft_append_resp*)resp)[o] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
+            ((raft_append_resp*)resp)[oc] = raft_append_resp{rt, ib(su) ? 1 : 0, ib(thrown) ? 1 : 0};
         } else {
-            append_command<TB, true>(x.ref(), __ballot(1), lv, ((const uint32_t*)req)[o], cnt);
+            append_command<TB, true>(x.ref(), __ballot(1), lv, qm, cnt);
         }
         drew |= resolve_rep_draw(x, p, t, gid, r);
+        if (!more(++m)) break;
     }
     store_rep<VO>(x, o, drew, p, idx);
     if (cnt.miss) atomicAdd(&flags[1], cnt.miss);
@@ -990,6 +1001,7 @@ constexpr int BUCKET_MEAN = 320;                                        // targe
 // (per 10^6-message batch, 512 threads at 320 per bucket beat 256 at 160 and
 // 1,024 at 640 by 5-10 %, profiles/r5_h)
 constexpr int BUCKET_THREADS = 512;
+constexpr int GATHER_TILES = 2 * BUCKET_THREADS;                        // bucket_batch_kernel's direct gather
 
 // Wave w of the tile's workgroup takes messages [w * 64 * TILE_IPT, (w + 1) *
 // 64 * TILE_IPT) of it, 64 consecutive ones per round.  A message's place in
@@ -1098,6 +1110,7 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
                                                           const uint2* __restrict__ tiles,
                                                           const uint2* __restrict__ seg, const void* req,
                                                           void* resp, unsigned int* flags) {
+    static_assert(2 * NT >= GATHER_TILES, "the direct gather holds at most two tiles per thread");
     using Sort = rocprim::block_radix_sort<uint32_t, NT, 1, uint32_t>;
     using Scan = rocprim::block_scan<uint32_t, NT>;
     __shared__ union {
@@ -1106,29 +1119,62 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
     } sm;
     __shared__ uint2 buf[NT];
     __shared__ uint32_t lk[NT], lo[NT];
+    __shared__ uint32_t spos[GATHER_TILES], soff[GATHER_TILES];
     if (*(volatile unsigned int*)&flags[0]) return;                   // the same for the whole grid
     const int bk = blockIdx.x;
     const uint32_t kb = (uint32_t)bk << S;
     // this thread's tiles [tt0, tt1): their segments of this bucket, and
     // where they start in the bucket's batch order
     const int per = (ntile + NT - 1) / NT, tt0 = threadIdx.x * per, tt1 = min(ntile, tt0 + per);
+    // up to GATHER_TILES tiles, their segments' starts and offsets go to LDS
+    // and every message of a chunk is fetched by its own thread (a binary
+    // search for its tile): one round trip.  (A thread walking its tiles'
+    // segments waits for each message in turn.)
+    const bool direct = ntile <= GATHER_TILES;
     uint32_t mine = 0;
-    for (int q = tt0; q < tt1; ++q) mine += seg[(int64_t)q * NB + bk].y;
+    uint2 sg0 = make_uint2(0u, 0u), sg1 = make_uint2(0u, 0u);
+    if (direct) {                                                       // per <= 2
+        if (tt0 < tt1) sg0 = seg[(int64_t)tt0 * NB + bk];
+        if (tt0 + 1 < tt1) sg1 = seg[(int64_t)(tt0 + 1) * NB + bk];
+        mine = sg0.y + sg1.y;
+    } else {
+        for (int q = tt0; q < tt1; ++q) mine += seg[(int64_t)q * NB + bk].y;
+    }
     uint32_t pos, len_all;
     Scan().exclusive_scan(mine, pos, 0u, len_all, sm.scan, rocprim::plus<uint32_t>());
+    if (direct) {
+        if (tt0 < tt1) { spos[tt0] = pos; soff[tt0] = sg0.x; }
+        if (tt0 + 1 < tt1) { spos[tt0 + 1] = pos + sg0.y; soff[tt0 + 1] = sg1.x; }
+    }
     for (uint32_t c0 = 0; c0 < len_all; c0 += NT) {                  // workgroup-uniform
         const int len = (int)min(len_all - c0, (uint32_t)NT);
-        // the chunk's messages [c0, c0 + len) of the bucket into buf, in batch order
-        uint32_t at = pos;
-        for (int q = tt0; q < tt1 && at < c0 + len; ++q) {
-            const uint2 sg = seg[(int64_t)q * NB + bk];
-            const uint32_t lo_i = max(at, c0), hi_i = min(at + sg.y, c0 + (uint32_t)len);
-            for (uint32_t i = lo_i; i < hi_i; ++i) buf[i - c0] = tiles[(int64_t)q * TILE + sg.x + (i - at)];
-            at += sg.y;
+        if (!direct) {
+            // the chunk's messages [c0, c0 + len) of the bucket into buf, in batch order
+            uint32_t at = pos;
+            for (int q = tt0; q < tt1 && at < c0 + len; ++q) {
+                const uint2 sg = seg[(int64_t)q * NB + bk];
+                const uint32_t lo_i = max(at, c0), hi_i = min(at + sg.y, c0 + (uint32_t)len);
+                for (uint32_t i = lo_i; i < hi_i; ++i) buf[i - c0] = tiles[(int64_t)q * TILE + sg.x + (i - at)];
+                at += sg.y;
+            }
         }
-        __syncthreads();                                                // buf complete (and sm.scan / sm.sort free)
+        __syncthreads();                                                // buf / spos complete (sm.scan / sm.sort free)
         const int q = threadIdx.x;
-        const uint2 x = q < len ? buf[q] : make_uint2(kb + (1u << S), 0u);   // padding sorts last
+        uint2 x = make_uint2(kb + (1u << S), 0u);                      // padding sorts last
+        if (q < len) {
+            if (direct) {
+                // the last tile whose segment starts at or before position i
+                const uint32_t i = c0 + (uint32_t)q;
+                int lo_t = 0, hi_t = ntile;
+                while (hi_t - lo_t > 1) {
+                    const int mid = (lo_t + hi_t) >> 1;
+                    if (spos[mid] <= i) lo_t = mid; else hi_t = mid;
+                }
+                x = tiles[(int64_t)lo_t * TILE + soff[lo_t] + (i - spos[lo_t])];
+            } else {
+                x = buf[q];
+            }
+        }
         uint32_t k[1] = {x.x - kb}, v[1] = {x.y};
         Sort().sort(k, v, sm.sort, 0, S + 1);
         lk[q] = k[0];

@@ -796,6 +796,17 @@ def test_handler_batches_skewed_vs_oracle():
     check_handler_batches(R, G, cap, 0, abi.MODE_REFERENCE, w, lt, lc, grp, dst, vq, aq, cmd)
 
 
+@pytest.mark.parametrize("n", [1, 2, 63, 65, 4095, 4097])
+def test_handler_batches_ragged_sizes_vs_oracle(n):
+    """Batch sizes around the bucketed path's wave (64) and tile (4096)
+    boundaries, a single message included: both paths against the oracle."""
+    rng = np.random.default_rng(41 + n)
+    R, G, cap = 5, 50, 8
+    w, lt, lc = random_states(rng, G, R, cap)
+    grp, dst, vq, aq, cmd = handler_messages(rng, n, G, R, cap)
+    check_handler_batches(R, G, cap, 0, abi.MODE_REFERENCE, w, lt, lc, grp, dst, vq, aq, cmd)
+
+
 def test_batch_paths_agree_at_scale():
     """4.2·10^6 votes over 10^6 groups of 5 (the bucketed path's bucket-count
     cap applies: S is raised until at most 16384 buckets remain), then 10^6
