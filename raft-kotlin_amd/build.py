@@ -7,8 +7,9 @@ every source and header the library is compiled from plus the compiler flags,
 the id is compiled into the library (`raft_build_source_id()`) and written
 beside it (`libraft_engine.so.srcid`), and a build whose id differs from the
 working tree's is rebuilt here and refused by `abi.load_library`.  The step
-kernel's own id (`kernel_source_id()`, the three kernel sources; bench.py keys
-its rocprofv3 rows on it) is compiled in too (`raft_build_kernel_source_id()`).
+kernel's own id (`kernel_source_id()`, the step kernel's sources -- not the
+handler batches' raft_batch.hip; bench.py keys its rocprofv3 rows on it) is
+compiled in too (`raft_build_kernel_source_id()`).
 """
 from __future__ import annotations
 
@@ -21,12 +22,15 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 SRC = os.path.join(CSRC, "raft_engine.hip")
-SRCS = [SRC, os.path.join(CSRC, "raft_wire.cpp"),                   # the wire codec is host code
+SRCS = [SRC, os.path.join(CSRC, "raft_batch.hip"),                   # the handler batches
+        os.path.join(CSRC, "raft_wire.cpp"),                         # the wire codec is host code
         os.path.join(CSRC, "raft_host.cpp"),                         # page-locked batch memory
         os.path.join(CSRC, "raft_comm.cpp")]                         # the RCCL counter all-reduce (dlopen)
-HDRS = [os.path.join(CSRC, h) for h in ("raft_step.h", "philox.h")] + [
+HDRS = [os.path.join(CSRC, h) for h in ("raft_step.h", "philox.h", "raft_engine_impl.h")] + [
     os.path.join(ROOT, "include", h) for h in ("raft_engine.h", "raft_wire.h")]
-KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h")     # bench.py kernel_source_id
+# the step kernel's sources (bench.py's kernel_source_id, the key of its
+# rocprofv3 rows): not raft_batch.hip, which holds no step-kernel code
+KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h", "raft_engine_impl.h")
 OUT = os.path.join(PKG, "lib", "libraft_engine.so")
 ARCH = os.environ.get("RAFT_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", "-ldl"]

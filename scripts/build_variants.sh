@@ -28,6 +28,7 @@ build_one() {
   done
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -munsafe-fp-atomics -I "$d/include" $flags \
       -o "raft-kotlin_amd/lib/libraft_engine_$name.so" "$d/raft-kotlin_amd/csrc/raft_engine.hip" \
+      $( [ -f "$d/raft-kotlin_amd/csrc/raft_batch.hip" ] && echo "$d/raft-kotlin_amd/csrc/raft_batch.hip" ) \
       "$d/raft-kotlin_amd/csrc/raft_wire.cpp" $( [ -f "$d/raft-kotlin_amd/csrc/raft_host.cpp" ] && echo "$d/raft-kotlin_amd/csrc/raft_host.cpp" ) \
       $( [ -f "$d/raft-kotlin_amd/csrc/raft_comm.cpp" ] && echo "$d/raft-kotlin_amd/csrc/raft_comm.cpp -ldl" )
   rm -rf "$d"
