@@ -233,6 +233,7 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
 constexpr int TILE_IPT = 16, TILE = BLOCK * TILE_IPT;
 constexpr int BUCKETS_MAX = 3072;                                       // bucket_tile_kernel's LDS: TILE * 8 + 5 * NB * 2 < 64 KB
 constexpr int BUCKET_MEAN = 320;                                        // target messages per bucket
+constexpr uint64_t SEG_MAX = 1ull << 27;                                // segment-table entries (1 GB)
 // bucket_batch_kernel's workgroup: a bucket's chunk, one message per thread
 // (per 10^6-message batch, 512 threads at 320 per bucket beat 256 at 160 and
 // 1,024 at 640 by 5-10 %, profiles/r5_h)
@@ -486,11 +487,15 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
                              void* resp, int n, uint64_t nkeys) {
     int S = 0;
     while (S < 31 && ((uint64_t)n << S) < (uint64_t)BUCKET_MEAN * nkeys) ++S;
-    while (S < 31 && ((nkeys + (1ull << S) - 1) >> S) > (uint64_t)BUCKETS_MAX) ++S;
-    const int NB = (int)((nkeys + (1ull << S) - 1) >> S);
+    // at most BUCKETS_MAX buckets, and a segment table (NB x ntile entries of
+    // 8 B) of at most SEG_MAX entries: very large batches take larger buckets
+    const uint64_t ntile64 = ((uint64_t)n + TILE - 1) / TILE;
+    auto nb_of = [&](int s) { return (nkeys + (1ull << s) - 1) >> s; };
+    while (S < 31 && (nb_of(S) > (uint64_t)BUCKETS_MAX || nb_of(S) * ntile64 > SEG_MAX)) ++S;
+    const int NB = (int)nb_of(S);
     int bbits = 1;
     while ((uint64_t)(NB - 1) >> bbits) ++bbits;
-    const int ntile = (n + TILE - 1) / TILE;
+    const int ntile = (int)ntile64;
     const size_t b_t = al256((size_t)ntile * TILE * 8), b_s = al256((size_t)NB * ntile * 8);
     if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, b_t + b_s + 256)) return rc;
     char* b = e->bst;
