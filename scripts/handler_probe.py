@@ -45,7 +45,8 @@ def main():
             fn(d_group.data_ptr(), d_dst.data_ptr(), d_req.data_ptr(), d_resp.data_ptr(), N)
         plan.append([kind, REPS])
     e.close()
-    print(json.dumps({"n": N, "batch_path": PATH, "groups": G, "replicas": R, "kernel_src": bench.kernel_source_id(), "plan": plan}))
+    print(json.dumps({"n": N, "batch_path": PATH, "groups": G, "replicas": R, "kernel_src": bench.kernel_source_id(),
+                      "library_src": bench.library_source_id(), "plan": plan}))
 
 
 if __name__ == "__main__":

@@ -99,7 +99,8 @@ def main(d):
         hfetch, hwrite = avg(fb, hk) * 1024 * ff, avg(wb, hk) * 1024 * wf
         t_all, t_h = avg(tb) / 1e6, avg(tb, hk) / 1e6
         rows.append({"kind": kind, "n": n, "groups": plan["groups"], "replicas": plan["replicas"],
-                     "kernel_src": plan["kernel_src"], "batch_path": plan.get("batch_path", 0),
+                     "kernel_src": plan["kernel_src"], "library_src": plan.get("library_src"),
+                     "batch_path": plan.get("batch_path", 0),
                      "batches_averaged": len(ix),
                      "hbm_bytes_per_batch": fetch + write, "hbm_bytes_per_message": (fetch + write) / n,
                      "handler_kernel_hbm_bytes_per_message": (hfetch + hwrite) / n,
@@ -119,7 +120,7 @@ def merge(files):
         have = json.load(open(OUT_FILE))
     except (OSError, ValueError):
         have = []
-    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"], r["kernel_src"])  # noqa: E731
+    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"], r.get("library_src") or r["kernel_src"])  # noqa: E731
     out = {key(r): r for r in have}
     for f in files:
         for r in json.load(open(f)):
