@@ -456,7 +456,9 @@ def handler_parity(eng, O, params_kw, log_cap, kind, G, R, n_msgs, span, seed):
 def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
     """The drop-in service path (RaftServer.vote() / append(), RaftServer.kt:228-287):
     raft_vote_batch_dev / raft_append_batch_dev on n random messages already
-    in HBM (key, stable radix sort, one lane per replica run), and the same
+    in HBM (the bucketed path: a stable partition of each tile into buckets of
+    consecutive replicas, a workgroup per bucket sorting its messages in LDS,
+    one lane per replica run), and the same
     through the host entry points (from pageable arrays through pinned
     staging, and from page-locked arrays by direct DMA).  Parity: a batch of
     --handler-parity messages of each kind on a span of groups against the
@@ -533,8 +535,9 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
                                   "pmc_source": pmc["source"] if pmc else None},
                      "parity_messages": msgs, "parity_span_groups": min(G, args.handler_span),
                      "parity_mismatches": int(bad)}
-    out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a key kernel, a stable rocprim onesweep "
-                   "radix sort over the key bits, the handler kernel (one lane per replica run, messages in batch order) and "
+    out["note"] = ("raft_*_batch_dev on HBM-resident messages: per call a tile kernel (each tile's messages "
+                   "partitioned stably into buckets of consecutive replicas), the handler kernel (a workgroup per bucket: "
+                   "its messages gathered in batch order, sorted by replica in LDS, one lane per replica run) and "
                    "one status synchronisation; _host_buffers: the same through the host entry points from pageable "
                    "arrays (multi-threaded copy into engine-owned pinned staging, PCIe both ways); _pinned_host: from "
                    "page-locked arrays, which the DMA reads and writes directly. The engine holds the bench run's "
