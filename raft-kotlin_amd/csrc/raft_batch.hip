@@ -230,7 +230,10 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
 // messages keep batch order across chunks too.  Nothing global is scanned or
 // scattered: the only cross-tile step is each bucket's scan of its ntile
 // counts.
-constexpr int TILE_IPT = 16, TILE = BLOCK * TILE_IPT;
+#ifndef RAFT_TILE_IPT
+#define RAFT_TILE_IPT 16                                                // messages per thread of a tile (build-time)
+#endif
+constexpr int TILE_IPT = RAFT_TILE_IPT, TILE = BLOCK * TILE_IPT;
 constexpr int BUCKETS_MAX = 3072;                                       // bucket_tile_kernel's LDS: TILE * 8 + 5 * NB * 2 < 64 KB
 constexpr int BUCKET_MEAN = 320;                                        // target messages per bucket
 constexpr uint64_t SEG_MAX = 1ull << 27;                                // segment-table entries (1 GB)

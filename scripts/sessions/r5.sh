@@ -136,6 +136,13 @@ case $P in
       HANDLER_PATH=1 HANDLER_REPS=3 step htrace_sorted 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_sorted -o run --output-format csv -- python -u scripts/handler_probe.py
       step bench_handler 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0
       ;;
+  t)  # the native all-reduce test; handler batches with tiles of 2,048 (VARIANT tile8) vs 4,096
+      step pytest 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -v -k "native" --timeout 300 --timeout-method thread
+      for i in 1 2; do
+        HANDLER_REPS=3 step htrace_prod_$i 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_prod_$i -o run --output-format csv -- python -u scripts/handler_probe.py
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_tile8.so HANDLER_REPS=3 step htrace_tile8_$i 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_tile8_$i -o run --output-format csv -- python -u scripts/handler_probe.py
+      done
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh

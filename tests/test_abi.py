@@ -78,6 +78,23 @@ def test_create_without_gpu_fails_loudly(lib):
         eng.RaftEngine(abi.make_params(G=4))
 
 
+def test_comm_rejects_bad_arguments_before_loading_rccl(lib):
+    """raft_comm_create checks its arguments before RCCL is loaded or a device
+    touched (include/raft_engine.h raft_comm_*): a rank outside 0..nranks-1,
+    null pointers, and (in the wrapper) an id of the wrong length."""
+    eng = importlib.import_module("raft-kotlin_amd.engine")
+    uid = bytes(abi.COMM_ID_BYTES)
+    for nranks, rank in ((2, 2), (2, -1), (0, 0)):
+        with pytest.raises(eng.RaftError, match="rank outside"):
+            eng.RaftComm(uid, nranks, rank, 0)
+    with pytest.raises(ValueError):
+        eng.RaftComm(uid[:-1], 1, 0, 0)
+    h = C.c_void_p()
+    assert lib.raft_comm_create(None, 1, 0, 0, C.byref(h)) == abi.RAFT_EINVAL
+    assert lib.raft_comm_get_unique_id(None) == abi.RAFT_EINVAL
+    assert lib.raft_comm_destroy(None) == abi.RAFT_OK
+
+
 def _unbound_engine(R=5, cap=8):
     """A RaftEngine shell without a device handle: the argument checks of the
     batch wrappers run before any library call."""

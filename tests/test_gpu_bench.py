@@ -61,3 +61,33 @@ def test_forced_collective_at_one_rank(backend, mode, monkeypatch):
     co = o.step(warm + steps, nthreads=min(16, os.cpu_count() or 1))[:, : abi.NUM_COUNTERS]
     assert np.array_equal(res["warmup_counters"], co[:warm])
     assert np.array_equal(ca, co[warm:]), "all-reduced counter rows differ from the oracle's"
+
+
+def test_native_counter_allreduce_at_one_rank():
+    """raft_engine_allreduce_counters on a one-rank communicator of the
+    engine's own (raft_comm_*): out of place and in place it returns the rows
+    it was given, ordered after the engine's step launches on its stream; zero
+    rows is a no-op."""
+    import torch
+    eng_mod = importlib.import_module("raft-kotlin_amd.engine")
+    e = eng_mod.RaftEngine(abi.make_params(**dict(abi.CONFIGS[3], G=2000)))
+    comm = eng_mod.RaftComm(eng_mod.RaftComm.unique_id(), 1, 0, 0)
+    try:
+        dev = torch.device("cuda", 0)
+        n = 30
+        rows = torch.zeros((n, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+        out = torch.full_like(rows, -7)
+        torch.cuda.synchronize(dev)
+        e.step_async(n, rows.data_ptr())
+        e.allreduce_counters(comm, rows.data_ptr(), out.data_ptr(), n)
+        e.sync()
+        assert int(rows.abs().sum()) > 0
+        assert torch.equal(out, rows), "out of place"
+        keep = rows.clone()
+        e.allreduce_counters(comm, rows.data_ptr(), rows.data_ptr(), n)
+        e.allreduce_counters(comm, rows.data_ptr(), out.data_ptr(), 0)
+        e.sync()
+        assert torch.equal(rows, keep), "in place"
+    finally:
+        comm.close()
+        e.close()
