@@ -143,6 +143,20 @@ case $P in
         RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_tile8.so HANDLER_REPS=3 step htrace_tile8_$i 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_tile8_$i -o run --output-format csv -- python -u scripts/handler_probe.py
       done
       ;;
+  o)  # the other workloads at the final build (config 5, config 2, textbook config 3), the 1/8 shard
+      # plain and with the native one-rank all-reduce, and the N = 2 rehearsal (gloo ranks on one GPU)
+      step cfg5 300 python -u bench.py --config 5 --groups 100000 --no-cpu-baseline --handler-batch 0
+      step cfg2 300 python -u bench.py --config 2 --groups 10000 --no-cpu-baseline --handler-batch 0
+      step textbook 300 python -u bench.py --mode textbook --no-cpu-baseline --handler-batch 0
+      for i in 1 2; do
+        step s8_plain_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_native_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      done
+      TAG=r5_o/dist STEPS=512 step dist 900 bash scripts/dist_rehearsal.sh
+      for f in $OUT/*.log; do
+        echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"frac": [0-9.]*' $f | head -1)"
+      done > $OUT/summary.txt
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
