@@ -258,8 +258,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10_000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--groups", type=int, default=1_000_000,
-                    help="total groups (strong scaling) or groups per GPU (weak scaling)")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="total groups (strong scaling) or groups per GPU (weak scaling); default: the "
+                         "configuration's own (BASELINE.json: 10^6 for config 3, 10^5 for 5, 10^4 for 2)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong (config 4, BASELINE.json configs[3]): --groups split over the GPUs; weak: --groups "
                          "per GPU")
@@ -317,7 +318,10 @@ def parse_args(argv=None):
                          "calibrating rocprofv3's FETCH_SIZE / WRITE_SIZE in the same process (scripts/pmc_bench.sh)")
     ap.add_argument("--plan-only", action="store_true",
                     help="no GPU: start the ranks, agree on the shards over gloo, print them (tests)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.groups is None:
+        args.groups = abi.CONFIGS[args.config]["G"]
+    return args
 
 
 def cpu_baseline(args, kw, log_cap, total_steps):
