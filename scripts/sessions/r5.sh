@@ -157,6 +157,9 @@ case $P in
         echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"frac": [0-9.]*' $f | head -1)"
       done > $OUT/summary.txt
       ;;
+  ph)  # the handler batches' PMC rows alone (scripts/pmc_handler.sh) at the working tree's library
+      TAG=r5_${TAGP:-ph} step pmc_handler 600 bash scripts/pmc_handler.sh
+      ;;
   pmc)  # the PMC rows (scripts/pmc_bench.sh) of both bench commands at the working tree's kernel
       TAG=r5_${TAGP:-pmc}_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
       TAG=r5_${TAGP:-pmc}_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
