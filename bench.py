@@ -76,9 +76,14 @@ def kernel_source_id() -> str:
 
 
 def library_source_id() -> str:
-    """Short hash of everything the library is built from (the handler
-    batches' PMC rows are keyed on it: their kernels are not the step kernel's)."""
+    """Short hash of everything the library is built from."""
     return importlib.import_module("raft-kotlin_amd.build").library_source_id()
+
+
+def batch_source_id() -> str:
+    """Short hash of the handler batches' sources: their PMC rows are keyed on
+    it (their kernels are not the step kernel's)."""
+    return importlib.import_module("raft-kotlin_amd.build").batch_source_id()
 
 
 def shard(total: int, world: int, rank: int, scaling: str) -> tuple[int, int]:
@@ -482,7 +487,7 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         pmc_rows = json.load(open(HANDLER_PMC_FILE))
     except (OSError, ValueError):
         pmc_rows = []
-    src = library_source_id()
+    src = batch_source_id()
     out = {"messages_per_batch": n, "groups": G, "replicas": R}
     for kind, req, resp_w in (("vote", vote, 2), ("append", app, 3)):
         msgs, bad = handler_parity(eng, O, params_kw, log_cap, kind, G, R, args.handler_parity,
@@ -520,7 +525,7 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         dt_pin = time.perf_counter() - t0
         rate = n * args.handler_reps / dt_dev
         ach = HANDLER_ALG_BYTES[kind] * rate / 1e9
-        pmc = next((r for r in pmc_rows if (r["kind"], r["n"], r["groups"], r["replicas"], r.get("library_src"))
+        pmc = next((r for r in pmc_rows if (r["kind"], r["n"], r["groups"], r["replicas"], r.get("batch_src"))
                     == (kind, n, G, R, src)), None)
         out[kind] = {"messages_per_s_device": rate,
                      "ms_per_batch_device": dt_dev * 1e3 / args.handler_reps,

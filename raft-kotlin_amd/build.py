@@ -31,6 +31,9 @@ HDRS = [os.path.join(CSRC, h) for h in ("raft_step.h", "philox.h", "raft_engine_
 # the step kernel's sources (bench.py's kernel_source_id, the key of its
 # rocprofv3 rows): not raft_batch.hip, which holds no step-kernel code
 KERNEL_SOURCES = ("raft_step.h", "raft_engine.hip", "philox.h", "raft_engine_impl.h")
+# the handler batches' sources (bench.py keys their rocprofv3 rows on them)
+BATCH_SOURCES = [os.path.join(CSRC, f) for f in ("raft_batch.hip", "raft_engine_impl.h", "raft_step.h", "philox.h")] + [
+    os.path.join(ROOT, "include", "raft_engine.h")]
 OUT = os.path.join(PKG, "lib", "libraft_engine.so")
 ARCH = os.environ.get("RAFT_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics", "-ldl"]
@@ -41,6 +44,15 @@ def kernel_source_id() -> str:
     h = hashlib.sha1()
     for f in KERNEL_SOURCES:
         with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
+def batch_source_id() -> str:
+    """Short hash of the handler batches' sources (bench.py's key of their PMC rows)."""
+    h = hashlib.sha1()
+    for f in BATCH_SOURCES:
+        with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]
 

@@ -46,7 +46,8 @@ def main():
         plan.append([kind, REPS])
     e.close()
     print(json.dumps({"n": N, "batch_path": PATH, "groups": G, "replicas": R, "kernel_src": bench.kernel_source_id(),
-                      "library_src": bench.library_source_id(), "plan": plan}))
+                      "library_src": bench.library_source_id(), "batch_src": bench.batch_source_id(),
+                      "plan": plan}))
 
 
 if __name__ == "__main__":

@@ -100,6 +100,7 @@ def main(d):
         t_all, t_h = avg(tb) / 1e6, avg(tb, hk) / 1e6
         rows.append({"kind": kind, "n": n, "groups": plan["groups"], "replicas": plan["replicas"],
                      "kernel_src": plan["kernel_src"], "library_src": plan.get("library_src"),
+                     "batch_src": plan.get("batch_src"),
                      "batch_path": plan.get("batch_path", 0),
                      "batches_averaged": len(ix),
                      "hbm_bytes_per_batch": fetch + write, "hbm_bytes_per_message": (fetch + write) / n,
@@ -120,7 +121,8 @@ def merge(files):
         have = json.load(open(OUT_FILE))
     except (OSError, ValueError):
         have = []
-    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"], r.get("library_src") or r["kernel_src"])  # noqa: E731
+    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"],  # noqa: E731
+                     r.get("batch_src") or r.get("library_src") or r["kernel_src"])
     out = {key(r): r for r in have}
     for f in files:
         for r in json.load(open(f)):
