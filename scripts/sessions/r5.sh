@@ -157,6 +157,9 @@ case $P in
         echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"frac": [0-9.]*' $f | head -1)"
       done > $OUT/summary.txt
       ;;
+  v)  # the driver's bench command on the committed tree: every PMC-derived field attached?
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      ;;
   ph)  # the handler batches' PMC rows alone (scripts/pmc_handler.sh) at the working tree's library
       TAG=r5_${TAGP:-ph} step pmc_handler 600 bash scripts/pmc_handler.sh
       ;;
