@@ -114,6 +114,7 @@ int raft_engine_allreduce_counters(raft_engine* e, raft_comm* c, const int64_t* 
     if (!e || !c || !counters_dev || !out_dev || n_steps < 0) return raft_internal_fail(RAFT_EINVAL, "bad argument");
     if (n_steps == 0) return RAFT_OK;
     const Rccl& r = rccl();
+    if (!r.h) return raft_internal_fail(RAFT_ENODEV, r.err);    // (a communicator implies RCCL; defensive)
     if (hipSetDevice(c->device) != hipSuccess) return raft_internal_fail(RAFT_EDEVICE, "hipSetDevice failed");
     const size_t count = (size_t)n_steps * RAFT_COUNTER_STRIDE;
     if (ncclResult_t rc = r.all_reduce(counters_dev, out_dev, count, ncclInt64, ncclSum, c->comm,
