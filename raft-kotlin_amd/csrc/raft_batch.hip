@@ -143,7 +143,8 @@ __global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __rest
 // flags[1]: accesses below the retained log window (RAFT_EWINDOW)
 template <bool TB, int kind, class More, class Ord>
 __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_t idx, int m0, More more, Ord ord,
-                                          const void* req, void* resp, unsigned int* flags) {
+                                          const void* req, void* resp, unsigned int* flags,
+                                          unsigned int* hmiss = nullptr) {
     using Req = std::conditional_t<kind == BATCH_VOTE, raft_vote_req,
                                    std::conditional_t<kind == BATCH_APPEND, raft_append_req, uint32_t>>;
     const int R = p.R;
@@ -196,7 +197,10 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
         if (!more(++m)) break;
     }
     store_rep<VO>(x, o, drew, p, idx);
-    if (cnt.miss) atomicAdd(&flags[1], cnt.miss);
+    if (cnt.miss) {
+        atomicAdd(&flags[1], cnt.miss);
+        if (hmiss) *(volatile unsigned int*)hmiss = 1u;                 // (bucket path: the host copies the count)
+    }
 }
 
 // The sorted path: one thread per sorted position; the first position of each
@@ -237,6 +241,7 @@ constexpr int TILE_IPT = RAFT_TILE_IPT, TILE = BLOCK * TILE_IPT;
 constexpr int BUCKETS_MAX = 3072;                                       // bucket_tile_kernel's LDS: TILE * 8 + 5 * NB * 2 < 64 KB
 constexpr int BUCKET_MEAN = 320;                                        // target messages per bucket
 constexpr uint64_t SEG_MAX = 1ull << 27;                                // segment-table entries (1 GB)
+constexpr size_t BST_HEAD = 256;                                        // the staging's head: the bucketed path's status words
 // bucket_batch_kernel's workgroup: a bucket's chunk, one message per thread
 // (per 10^6-message batch, 512 threads at 320 per bucket beat 256 at 160 and
 // 1,024 at 640 by 5-10 %, profiles/r5_h)
@@ -252,7 +257,8 @@ constexpr int GATHER_TILES = 2 * BUCKET_THREADS;                        // bucke
 __global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __restrict__ group,
                                                             const int32_t* __restrict__ dst, int n, int64_t G, int R,
                                                             int S, int NB, int bbits, uint2* __restrict__ tiles,
-                                                            uint2* __restrict__ seg, unsigned int* flags) {
+                                                            uint2* __restrict__ seg, unsigned int* dflags,
+                                                            unsigned int* hflags) {
     // LDS: the tile's output staged (written out coalesced: one 8-B store per
     // message to its place would cost a 32-B sector each), then the waves'
     // counts and the tile's bucket offsets, [WAVES_PER_BLOCK + 1][NB] (<= TILE)
@@ -286,7 +292,10 @@ __global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __res
         key[j] = in && ok ? (uint32_t)((uint64_t)gg[j] * (uint64_t)R + (uint64_t)dd[j]) : 0u;
         bad |= in && !ok;
     }
-    if (bad) atomicOr(&flags[0], 1u);
+    if (bad) {                                                          // (idempotent plain stores)
+        *(volatile unsigned int*)&dflags[0] = 1u;
+        *(volatile unsigned int*)&hflags[0] = 1u;
+    }
     __syncthreads();                                                    // the counts are zero
 #pragma unroll
     for (int j = 0; j < TILE_IPT; ++j) {
@@ -349,7 +358,7 @@ template <bool TB, int kind, int NT>
 __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t t, int n, int S, int NB, int ntile,
                                                           const uint2* __restrict__ tiles,
                                                           const uint2* __restrict__ seg, const void* req,
-                                                          void* resp, unsigned int* flags) {
+                                                          void* resp, unsigned int* dflags, unsigned int* hflags) {
     static_assert(2 * NT >= GATHER_TILES, "the direct gather holds at most two tiles per thread");
     using Sort = rocprim::block_radix_sort<uint32_t, NT, 1, uint32_t>;
     using Scan = rocprim::block_scan<uint32_t, NT>;
@@ -360,7 +369,8 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
     __shared__ uint2 buf[NT];
     __shared__ uint32_t lk[NT], lo[NT];
     __shared__ uint32_t spos[GATHER_TILES], soff[GATHER_TILES];
-    if (*(volatile unsigned int*)&flags[0]) return;                   // the same for the whole grid
+    // a message outside the engine (bucket_tile_kernel): nothing is applied
+    const bool bad = *(volatile unsigned int*)&dflags[0] != 0u;         // the same for the whole grid
     const int bk = blockIdx.x;
     const uint32_t kb = (uint32_t)bk << S;
     // this thread's tiles [tt0, tt1): their segments of this bucket, and
@@ -386,7 +396,7 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
         if (tt0 < tt1) { spos[tt0] = pos; soff[tt0] = sg0.x; }
         if (tt0 + 1 < tt1) { spos[tt0 + 1] = pos + sg0.y; soff[tt0 + 1] = sg1.x; }
     }
-    for (uint32_t c0 = 0; c0 < len_all; c0 += NT) {                  // workgroup-uniform
+    for (uint32_t c0 = 0; c0 < (bad ? 0u : len_all); c0 += NT) {    // workgroup-uniform
         const int len = (int)min(len_all - c0, (uint32_t)NT);
         if (!direct) {
             // the chunk's messages [c0, c0 + len) of the bucket into buf, in batch order
@@ -423,7 +433,8 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
         if (q < len && (q == 0 || lk[q - 1] != lk[q])) {
             const uint32_t key = lk[q];
             apply_run<TB, kind>(p, t, (int64_t)(kb + key), q, [&](int m) { return m < len && lk[m] == key; },
-                                [&](int m) { return lo[m]; }, req, resp, flags);
+                                [&](int m) { return lo[m]; }, req, resp, dflags + 1,    // misses -> dflags[2]
+                                hflags + 1);
         }
         // another chunk of this bucket: the barrier (a workgroup-scope fence:
         // one CU, one L1) makes this chunk's replica stores visible to it, and
@@ -449,8 +460,11 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
                                                        (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u,
                                                        (unsigned)bits, e->stream));
     const size_t b_keys = al256((size_t)n * sizeof(Key)), b_ord = al256((size_t)n * 4);
-    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, 2 * b_keys + 2 * b_ord + al256(sort_tmp) + 256)) return rc;
-    char* b = e->bst;
+    const size_t sz0 = e->bst_bytes;
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, BST_HEAD + 2 * b_keys + 2 * b_ord + al256(sort_tmp) + 256))
+        return rc;
+    if (e->bst_bytes != sz0) HIP_TRY(hipMemsetAsync(e->bst, 0, BST_HEAD, e->stream));   // (the bucketed path's words)
+    char* b = e->bst + BST_HEAD;
     Key* k_in = (Key*)b; b += b_keys;
     Key* k_out = (Key*)b; b += b_keys;
     uint32_t* o_in = (uint32_t*)b; b += b_ord;
@@ -475,7 +489,7 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
 }
 
 using BK = void (*)(DevParams, uint32_t, int, int, int, int, const uint2*, const uint2*, const void*, void*,
-                    unsigned int*);
+                    unsigned int*, unsigned int*);
 static BK bucket_kernel_of(int kind, bool tb) {
     constexpr int NT = BUCKET_THREADS;
     return kind == BATCH_VOTE     ? (tb ? bucket_batch_kernel<true, BATCH_VOTE, NT> : bucket_batch_kernel<false, BATCH_VOTE, NT>)
@@ -500,19 +514,35 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
     while ((uint64_t)(NB - 1) >> bbits) ++bbits;
     const int ntile = (int)ntile64;
     const size_t b_t = al256((size_t)ntile * TILE * 8), b_s = al256((size_t)NB * ntile * 8);
-    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, b_t + b_s + 256)) return rc;
-    char* b = e->bst;
+    const size_t sz0 = e->bst_bytes;                                    // grow_dev reallocates only to grow
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, BST_HEAD + b_t + b_s)) return rc;
+    char* b = e->bst + BST_HEAD;
     uint2* tiles = (uint2*)b; b += b_t;
     uint2* seg = (uint2*)b; b += b_s;
-    unsigned int* flags = (unsigned int*)b;
-    HIP_TRY(hipMemsetAsync(flags, 0, 8, e->stream));
+    // status words: dflags (device: [0] a message outside the engine, [2]
+    // the window misses), zero between batches; hflags = the engine's
+    // page-locked words [0], [1] (RAFT_ERANGE; "some miss was counted"),
+    // written by the kernels with plain stores and read after the
+    // synchronisation.  A batch without either needs no memset and no copy;
+    // one with them copies the count and resets the device words (rare).
+    unsigned int* dflags = (unsigned int*)e->bst;                       // at a fixed place: the staging's head
+    if (e->bst_bytes != sz0) HIP_TRY(hipMemsetAsync(dflags, 0, BST_HEAD, e->stream));
+    unsigned int* hflags = (unsigned int*)e->dp.status - 8;             // device view of bflags_host
+    e->bflags_host[0] = e->bflags_host[1] = 0u;
     bucket_tile_kernel<<<ntile, BLOCK, (size_t)TILE * 8 + (size_t)(WAVES_PER_BLOCK + 1) * NB * 2, e->stream>>>(
-        group, dst, n, e->p.G, e->p.R, S, NB, bbits, tiles, seg, flags);
+        group, dst, n, e->p.G, e->p.R, S, NB, bbits, tiles, seg, dflags, hflags);
     const BK kern = bucket_kernel_of(kind, e->p.mode == RAFT_MODE_TEXTBOOK);
-    kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, flags);
+    kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, dflags,
+                                               hflags);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->bflags_host, flags, 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->bflags_host[0] | e->bflags_host[1]) {
+        unsigned int w[4] = {0u, 0u, 0u, 0u};
+        HIP_TRY(hipMemcpy(w, dflags, 16, hipMemcpyDeviceToHost));
+        e->bflags_host[1] = w[2];                                       // the count, for RAFT_EWINDOW
+        HIP_TRY(hipMemsetAsync(dflags, 0, 16, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
     return RAFT_OK;
 }
 

@@ -807,6 +807,58 @@ def test_handler_batches_ragged_sizes_vs_oracle(n):
     check_handler_batches(R, G, cap, 0, abi.MODE_REFERENCE, w, lt, lc, grp, dst, vq, aq, cmd)
 
 
+@pytest.mark.parametrize("path", ["bucketed", "sorted"])
+def test_batch_status_between_batches(path):
+    """Each batch's status is its own: a batch with a message outside the
+    engine fails with RAFT_ERANGE and applies nothing; the batches before and
+    after it (of other sizes, which move the staging) apply exactly as the
+    oracle's handlers; on a log_window ring a batch that reads below the window
+    reports RAFT_EWINDOW, and the next batch reports nothing."""
+    pid = abi.BATCH_PATH_BUCKETED if path == "bucketed" else abi.BATCH_PATH_SORTED
+    rng = np.random.default_rng(53)
+    R, G, cap = 5, 300, 8
+    w, lt, lc = random_states(rng, G, R, cap)
+    e, o = pair(R=R, G=G, log_cap=cap, seed=3)
+    e.set_batch_path(pid)
+    for x in (e, o):
+        x.write_state(w)
+        x.write_log(lt, lc)
+    for n, bad in ((5000, False), (3000, True), (70_000, False), (40, False)):
+        grp, dst, vq, _, _ = handler_messages(rng, n, G, R, cap)
+        if bad:
+            grp = grp.copy()
+            grp[n // 3] = G
+            before = e.read_state()
+            with pytest.raises(RuntimeError, match="outside the engine"):
+                e.vote_batch(grp, dst, vq)
+            assert np.array_equal(e.read_state(), before), "a failed batch applied something"
+            continue
+        ve = e.vote_batch(grp, dst, vq)
+        vo = np.array([o.vote(int(g), int(d), *map(int, q)) for g, d, q in zip(grp, dst, vq)], dtype=np.int32)
+        assert np.array_equal(ve, vo), f"n={n}: vote responses differ"
+    assert_same_state(e.read_state(), o.read_state(), R, f"{path} after a failed batch")
+    # the ring: physLen = lastIndex = 100 with a 16-slot window
+    W, cap2 = 16, 200
+    r = RaftEngine(abi.make_params(R=R, G=4, log_cap=cap2, log_window=W, seed=3))
+    r.set_batch_path(pid)
+    w2 = blank_groups(4, R)
+    for q in range(R):
+        set_fld(w2, R, q, "phys", np.full(4, 100))
+        set_fld(w2, R, q, "last", np.full(4, 100))
+        set_fld(w2, R, q, "term", np.full(4, 3))
+    r.write_state(w2)
+    r.write_log(np.full((4, R, cap2), 3, dtype=np.int32), np.zeros((4, R, cap2), dtype=np.uint32))
+    n = 4 * R
+    grp, dst = np.repeat(np.arange(4), R), np.tile(np.arange(R), 4).astype(np.int32)
+    aq = np.zeros((n, 8), dtype=np.int64)
+    aq[:, 0], aq[:, 1], aq[:, 2], aq[:, 3] = 3, 1, 10, 3              # prevLogIndex 10: below physLen - W
+    with pytest.raises(RuntimeError, match=f"{n} log accesses below the retained log_window"):
+        r.append_batch(grp, dst, aq)
+    vq = np.zeros((n, 4), dtype=np.int32)
+    vq[:, 0], vq[:, 1], vq[:, 2], vq[:, 3] = 3, 1, 100, 3
+    r.vote_batch(grp, dst, vq)                                          # inside the window: no status left over
+
+
 def test_batch_paths_agree_at_scale():
     """4.2·10^6 votes over 10^6 groups of 5 (the bucketed path's bucket-count
     cap applies: S is raised until at most 16384 buckets remain), then 10^6
