@@ -157,7 +157,10 @@ case $P in
         echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"frac": [0-9.]*' $f | head -1)"
       done > $OUT/summary.txt
       ;;
-  v)  # the driver's bench command on the committed tree: every PMC-derived field attached?
+  v)  # the committed tree as the driver will run it: the GPU suite, smoke, the driver's bench
+      # command (every PMC-derived field attached?)
+      [ -n "${NOTESTS:-}" ] || step pytest 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+      [ -n "${NOTESTS:-}" ] || step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
       step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       ;;
   ph)  # the handler batches' PMC rows alone (scripts/pmc_handler.sh) at the working tree's library
