@@ -14,6 +14,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -234,11 +235,17 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
 // messages keep batch order across chunks too.  Nothing global is scanned or
 // scattered: the only cross-tile step is each bucket's scan of its ntile
 // counts.
-#ifndef RAFT_TILE_IPT
-#define RAFT_TILE_IPT 16                                                // messages per thread of a tile (build-time)
+// a tile's workgroup (build-time: 512 threads x 8 messages; 256 x 16 ran the
+// tile kernel at one wave per SIMD, 16 serial ballot rounds per wave)
+#ifndef RAFT_TILE_THREADS
+#define RAFT_TILE_THREADS 512
 #endif
-constexpr int TILE_IPT = RAFT_TILE_IPT, TILE = BLOCK * TILE_IPT;
-constexpr int BUCKETS_MAX = 3072;                                       // bucket_tile_kernel's LDS: TILE * 8 + 5 * NB * 2 < 64 KB
+#ifndef RAFT_TILE_IPT
+#define RAFT_TILE_IPT 8
+#endif
+constexpr int TILE_THREADS = RAFT_TILE_THREADS, TILE_WAVES = TILE_THREADS / 64;
+constexpr int TILE_IPT = RAFT_TILE_IPT, TILE = TILE_THREADS * TILE_IPT;
+constexpr int BUCKETS_MAX = 3072;                                       // bucket_tile_kernel's LDS: TILE * 8 + (TILE_WAVES + 1) * NB * 2
 constexpr int BUCKET_MEAN = 320;                                        // target messages per bucket
 constexpr uint64_t SEG_MAX = 1ull << 27;                                // segment-table entries (1 GB)
 constexpr size_t BST_HEAD = 256;                                        // the staging's head: the bucketed path's status words
@@ -254,20 +261,20 @@ constexpr int GATHER_TILES = 2 * BUCKET_THREADS;                        // bucke
 // match by ballots over the bucket bits), plus the wave's earlier rounds (the
 // wave's LDS count, read by every lane of the match and then advanced by its
 // lowest lane), plus the earlier waves (their counts, summed after the tile).
-__global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __restrict__ group,
+__global__ __launch_bounds__(TILE_THREADS) void bucket_tile_kernel(const int64_t* __restrict__ group,
                                                             const int32_t* __restrict__ dst, int n, int64_t G, int R,
                                                             int S, int NB, int bbits, uint2* __restrict__ tiles,
                                                             uint2* __restrict__ seg, unsigned int* dflags,
                                                             unsigned int* hflags) {
     // LDS: the tile's output staged (written out coalesced: one 8-B store per
     // message to its place would cost a 32-B sector each), then the waves'
-    // counts and the tile's bucket offsets, [WAVES_PER_BLOCK + 1][NB] (<= TILE)
+    // counts and the tile's bucket offsets, [TILE_WAVES + 1][NB] (<= TILE)
     extern __shared__ uint2 stage[];                                    // [TILE]
     uint16_t* const cnt = (uint16_t*)(stage + TILE);
-    for (int b = threadIdx.x; b < WAVES_PER_BLOCK * NB; b += BLOCK) cnt[b] = 0;
+    for (int b = threadIdx.x; b < TILE_WAVES * NB; b += TILE_THREADS) cnt[b] = 0;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint16_t* const cw = cnt + w * NB;
-    uint16_t* const off = cnt + WAVES_PER_BLOCK * NB;                    // the tile's bucket offsets
+    uint16_t* const off = cnt + TILE_WAVES * NB;                    // the tile's bucket offsets
     const uint64_t below = (1ull << lane) - 1ull;
     const int t0 = blockIdx.x * TILE;
     const int base = t0 + w * 64 * TILE_IPT + lane;
@@ -317,11 +324,11 @@ __global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __res
     // the waves' counts -> their prefixes; the tile's count per bucket, and
     // its exclusive scan over the buckets (each thread a contiguous range of
     // buckets, then a block scan of the ranges' sums)
-    const int per = (NB + BLOCK - 1) / BLOCK, b0 = threadIdx.x * per, b1 = min(NB, b0 + per);
+    const int per = (NB + TILE_THREADS - 1) / TILE_THREADS, b0 = threadIdx.x * per, b1 = min(NB, b0 + per);
     uint32_t sum = 0;
     for (int b = b0; b < b1; ++b) {
         uint32_t c = 0;
-        for (int q = 0; q < WAVES_PER_BLOCK; ++q) {
+        for (int q = 0; q < TILE_WAVES; ++q) {
             const uint32_t x = cnt[q * NB + b];
             cnt[q * NB + b] = (uint16_t)c;
             c += x;
@@ -330,7 +337,7 @@ __global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __res
         sum += c;
     }
     uint32_t pre;
-    rocprim::block_scan<uint32_t, BLOCK>().exclusive_scan(sum, pre, 0u);
+    rocprim::block_scan<uint32_t, TILE_THREADS>().exclusive_scan(sum, pre, 0u);
     for (int b = b0; b < b1; ++b) {
         const uint32_t c = off[b];
         off[b] = (uint16_t)pre;
@@ -348,7 +355,7 @@ __global__ __launch_bounds__(BLOCK) void bucket_tile_kernel(const int64_t* __res
     }
     __syncthreads();
     const int len = min(TILE, n - t0);
-    for (int q = threadIdx.x; 2 * q < len; q += BLOCK) {                 // two messages per 16-B store
+    for (int q = threadIdx.x; 2 * q < len; q += TILE_THREADS) {                 // two messages per 16-B store
         if (2 * q + 1 < len) *(uint4*)&tiles[t0 + 2 * q] = *(const uint4*)&stage[2 * q];
         else tiles[t0 + 2 * q] = stage[2 * q];
     }
@@ -529,7 +536,15 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
     if (e->bst_bytes != sz0) HIP_TRY(hipMemsetAsync(dflags, 0, BST_HEAD, e->stream));
     unsigned int* hflags = (unsigned int*)e->dp.status - 8;             // device view of bflags_host
     e->bflags_host[0] = e->bflags_host[1] = 0u;
-    bucket_tile_kernel<<<ntile, BLOCK, (size_t)TILE * 8 + (size_t)(WAVES_PER_BLOCK + 1) * NB * 2, e->stream>>>(
+    const size_t tile_lds = (size_t)TILE * 8 + (size_t)(TILE_WAVES + 1) * NB * 2;
+    // (more than 64 KB of dynamic LDS: allowed once per device)
+    static std::atomic<bool> lds_set[64];
+    if (e->device < 0 || e->device >= 64 || !lds_set[e->device].load(std::memory_order_acquire)) {
+        HIP_TRY(hipFuncSetAttribute((const void*)bucket_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)((size_t)TILE * 8 + (size_t)(TILE_WAVES + 1) * BUCKETS_MAX * 2)));
+        if (e->device >= 0 && e->device < 64) lds_set[e->device].store(true, std::memory_order_release);
+    }
+    bucket_tile_kernel<<<ntile, TILE_THREADS, tile_lds, e->stream>>>(
         group, dst, n, e->p.G, e->p.R, S, NB, bbits, tiles, seg, dflags, hflags);
     const BK kern = bucket_kernel_of(kind, e->p.mode == RAFT_MODE_TEXTBOOK);
     kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, dflags,

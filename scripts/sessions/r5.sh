@@ -136,6 +136,14 @@ case $P in
       HANDLER_PATH=1 HANDLER_REPS=3 step htrace_sorted 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_sorted -o run --output-format csv -- python -u scripts/handler_probe.py
       step bench_handler 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0
       ;;
+  t2)  # handler batches: the tile kernel at 512 x 8 (the build) vs 256 x 16 (VARIANT tile256)
+      step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "handler or batch" --timeout 300 --timeout-method thread
+      for i in 1 2; do
+        HANDLER_REPS=3 step htrace_prod_$i 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_prod_$i -o run --output-format csv -- python -u scripts/handler_probe.py
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_tile256.so HANDLER_REPS=3 step htrace_tile256_$i 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace_tile256_$i -o run --output-format csv -- python -u scripts/handler_probe.py
+      done
+      step bench_handler 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0
+      ;;
   t)  # the native all-reduce test; handler batches with tiles of 2,048 (VARIANT tile8) vs 4,096
       step pytest 600 python -u -m pytest tests/test_gpu_bench.py -m gpu -v -k "native" --timeout 300 --timeout-method thread
       for i in 1 2; do
@@ -156,6 +164,12 @@ case $P in
       for f in $OUT/*.log; do
         echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"frac": [0-9.]*' $f | head -1)"
       done > $OUT/summary.txt
+      ;;
+  fin)  # the handler PMC rows at the working tree's batch sources, then the final checks (preset v)
+      TAG=r5_${TAGP:-fin} step pmc_handler 600 bash scripts/pmc_handler.sh
+      step pytest 1500 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       ;;
   v)  # the committed tree as the driver will run it: the GPU suite, smoke, the driver's bench
       # command (every PMC-derived field attached?)
