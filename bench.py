@@ -300,6 +300,9 @@ def parse_args(argv=None):
                          "after the last launch, inside the timed region (end); per --reduce-every chunk, in series "
                          "with the launches (inline); or once the clock has stopped (after: a diagnostic that "
                          "leaves the collective off the clock)")
+    ap.add_argument("--sync", choices=["spin", "block"], default="block",
+                    help="how the host waits for the timed region's last work before the closing device sync: "
+                         "poll its event (spin) or the runtime's blocking wait alone (block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-general-leg", action="store_true",
                     help="N = 1: skip the general_kernel leg (the main leg on the run-time-decided kernel)")
@@ -487,7 +490,8 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         pmc_rows = json.load(open(HANDLER_PMC_FILE))
     except (OSError, ValueError):
         pmc_rows = []
-    src = batch_source_id()
+    src = abi.build_ids()["batch_source_id"]               # the loaded library's (its compile-time knobs included)
+    path = eng.batch_path
     out = {"messages_per_batch": n, "groups": G, "replicas": R}
     for kind, req, resp_w in (("vote", vote, 2), ("append", app, 3)):
         msgs, bad = handler_parity(eng, O, params_kw, log_cap, kind, G, R, args.handler_parity,
@@ -525,8 +529,8 @@ def handler_batch_leg(eng, args, params_kw, log_cap, dev, G, R):
         dt_pin = time.perf_counter() - t0
         rate = n * args.handler_reps / dt_dev
         ach = HANDLER_ALG_BYTES[kind] * rate / 1e9
-        pmc = next((r for r in pmc_rows if (r["kind"], r["n"], r["groups"], r["replicas"], r.get("batch_src"))
-                    == (kind, n, G, R, src)), None)
+        pmc = next((r for r in pmc_rows if (r["kind"], r["n"], r["groups"], r["replicas"], r.get("batch_src"),
+                                            r.get("batch_path", 0)) == (kind, n, G, R, src, path)), None)
         out[kind] = {"messages_per_s_device": rate,
                      "ms_per_batch_device": dt_dev * 1e3 / args.handler_reps,
                      "messages_per_s_host_buffers": n * reps_h / dt_host,
@@ -607,7 +611,10 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
         dist.barrier()
 
     # ---- timed region ----
-    eng.set_kernel_timing(True)
+    # RAFT_BENCH_NO_KERNEL_EVENTS=1 (an A/B of the launches' own timestamps,
+    # DESIGN.md §6): the launches carry none; the kernel times are then absent
+    timing = os.environ.get("RAFT_BENCH_NO_KERNEL_EVENTS") != "1"
+    eng.set_kernel_timing(timing)
     ev1 = torch.cuda.Event(enable_timing=True)
     ar0 = torch.cuda.Event(enable_timing=True)
     ar1 = torch.cuda.Event(enable_timing=True)
@@ -659,6 +666,12 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
                 dist.all_reduce(gcounters)
         ar1.record(stream)
     ev1.record(stream)
+    if args.sync == "spin":
+        # the host polls the region's last event before the closing device
+        # sync: a blocking wait sleeps on an interrupt once the runtime's short
+        # active wait times out, and wakes ~15 us after the GPU is done
+        while not ev1.query():
+            pass
     torch.cuda.synchronize(dev)                 # the device: the engine's streams and the counter all-reduce
     wall = time.perf_counter() - t0             # this rank's clock; the job's time is the MAX over ranks (below)
     if coll:
@@ -671,7 +684,7 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
             dist.all_reduce(gcounters)
             torch.cuda.synchronize(dev)
             after_ms = (time.perf_counter() - t_ar) * 1e3
-    ev_ms = eng.timed_span(ev1.cuda_event)
+    ev_ms = eng.timed_span(ev1.cuda_event) if timing else wall * 1e3
     allreduce_ms = ar0.elapsed_time(ar1) if mode == "end" else (after_ms if mode == "after" else None)
     kern_ms, launches = eng.kernel_time()
     eng.set_kernel_timing(False)

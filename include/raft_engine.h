@@ -263,9 +263,12 @@ int         raft_abi_version(void);
  * library_source_id; abi.load_library refuses a library whose id differs
  * from the sources beside it), and of the step kernel's three sources
  * (kernel_source_id, the key of bench.py's rocprofv3 rows).  "unknown" for a
- * build made without build.py. */
+ * build made without build.py.  raft_build_batch_source_id: the handler
+ * batches' sources and the compile-time knobs that shape their kernels
+ * (build.py batch_source_id, the key of their rocprofv3 rows). */
 const char* raft_build_source_id(void);
 const char* raft_build_kernel_source_id(void);
+const char* raft_build_batch_source_id(void);
 int raft_engine_create(const raft_params* p, int device, raft_engine** out);
 int raft_engine_destroy(raft_engine* e);
 
@@ -347,9 +350,13 @@ int raft_engine_allreduce_counters(raft_engine* e, raft_comm* c, const int64_t* 
  * every chunk's state into registers and back exactly as a step launch's
  * piece entry and exit does (values unchanged); kind 1 makes one 8-byte store
  * per replica into its own log row past its last entry (a flat log only), the
- * Log.add pattern (Commons.kt:56-68).  Returns the bytes the probe's one
+ * Log.add pattern (Commons.kt:56-68).  Kinds 2 and 3 calibrate the handler
+ * batches' scattered accesses: 2^21 threads each load (2) or store (3) one
+ * 4-byte word in its own 32-byte sector of a 512 MB engine-owned scratch
+ * (sectors spread by an odd multiplicative permutation; the state is not
+ * touched), counted as 32 bytes per sector.  Returns the bytes the probe's one
  * dispatch reads and writes, so FETCH_SIZE / WRITE_SIZE of that dispatch
- * give the counters' byte factors for the step kernel's own access widths. */
+ * give the counters' byte factors for the probed access pattern. */
 int raft_engine_traffic_probe(raft_engine* e, int32_t kind, int64_t* bytes_read, int64_t* bytes_written);
 int64_t raft_engine_device_bytes(raft_engine* e);
 int     raft_engine_trim_staging(raft_engine* e);

@@ -237,7 +237,8 @@ def build_ids() -> dict:
     """The loaded library's provenance (include/raft_engine.h raft_build_*)."""
     lib = load_library()
     return {"library_source_id": lib.raft_build_source_id().decode(),
-            "kernel_source_id": lib.raft_build_kernel_source_id().decode(), "path": LIB_PATH}
+            "kernel_source_id": lib.raft_build_kernel_source_id().decode(),
+            "batch_source_id": lib.raft_build_batch_source_id().decode(), "path": LIB_PATH}
 
 
 def load_library(path: str | None = None):
@@ -261,6 +262,7 @@ def load_library(path: str | None = None):
         "raft_abi_version": (C.c_int, []),
         "raft_build_source_id": (C.c_char_p, []),
         "raft_build_kernel_source_id": (C.c_char_p, []),
+        "raft_build_batch_source_id": (C.c_char_p, []),
         "raft_engine_create": (C.c_int, [P(raft_params), C.c_int, P(eng)]),
         "raft_engine_destroy": (C.c_int, [eng]),
         "raft_engine_step": (C.c_int, [eng, I32, P(I64)]),
@@ -332,7 +334,7 @@ def load_library(path: str | None = None):
 # symbols declared in include/*.h (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "raft_params_default", "raft_last_error", "raft_abi_version", "raft_build_source_id",
-    "raft_build_kernel_source_id", "raft_engine_create",
+    "raft_build_kernel_source_id", "raft_build_batch_source_id", "raft_engine_create",
     "raft_engine_destroy", "raft_engine_step", "raft_engine_step_async", "raft_engine_sync",
     "raft_engine_stream", "raft_engine_set_kernel_timing", "raft_engine_kernel_time", "raft_engine_timed_span",
     "raft_engine_step_index", "raft_engine_set_step_index", "raft_engine_set_steps_per_launch",

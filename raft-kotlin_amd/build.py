@@ -49,7 +49,10 @@ def kernel_source_id() -> str:
 
 
 def batch_source_id() -> str:
-    """Short hash of the handler batches' sources (bench.py's key of their PMC rows)."""
+    """Short hash of the handler batches' sources.  The library reports it
+    with its kernels' compile-time knobs appended (raft_build_batch_source_id,
+    e.g. "<hash>-t512x8"): bench.py keys their PMC rows on the loaded
+    library's id, so a variant build never matches a production row."""
     h = hashlib.sha1()
     for f in BATCH_SOURCES:
         with open(f, "rb") as fh:
@@ -99,9 +102,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(f"{OUT} is current (sources {library_source_id()})", flush=True)
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    sid, kid = library_source_id(), kernel_source_id()
+    sid, kid, bid = library_source_id(), kernel_source_id(), batch_source_id()
     cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, f'-DRAFT_BUILD_SOURCE_ID="{sid}"',
-           f'-DRAFT_BUILD_KERNEL_ID="{kid}"', "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", *SRCS]
+           f'-DRAFT_BUILD_KERNEL_ID="{kid}"', f'-DRAFT_BUILD_BATCH_ID="{bid}"', "-I", os.path.join(ROOT, "include"),
+           "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

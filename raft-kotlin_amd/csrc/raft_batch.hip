@@ -533,7 +533,10 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
     // synchronisation.  A batch without either needs no memset and no copy;
     // one with them copies the count and resets the device words (rare).
     unsigned int* dflags = (unsigned int*)e->bst;                       // at a fixed place: the staging's head
-    if (e->bst_bytes != sz0) HIP_TRY(hipMemsetAsync(dflags, 0, BST_HEAD, e->stream));
+    // new staging, or an earlier batch that returned an error after its
+    // kernels were enqueued (its words may still be set): zero them first
+    if (e->bst_bytes != sz0 || e->bst_dirty) HIP_TRY(hipMemsetAsync(dflags, 0, BST_HEAD, e->stream));
+    e->bst_dirty = true;                                                // until this batch ends cleanly
     unsigned int* hflags = (unsigned int*)e->dp.status - 8;             // device view of bflags_host
     e->bflags_host[0] = e->bflags_host[1] = 0u;
     const size_t tile_lds = (size_t)TILE * 8 + (size_t)(TILE_WAVES + 1) * NB * 2;
@@ -558,6 +561,7 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
         HIP_TRY(hipMemsetAsync(dflags, 0, 16, e->stream));
         HIP_TRY(hipStreamSynchronize(e->stream));
     }
+    e->bst_dirty = false;
     return RAFT_OK;
 }
 
@@ -673,6 +677,18 @@ static int run_batch_on_device(raft_engine* e, int kind, const int64_t* group, c
 }
 
 extern "C" {
+
+// the handler batches' provenance: build.py's batch_source_id plus the
+// compile-time knobs of their kernels, so a variant build's rocprofv3 rows
+// never carry the production build's key
+#ifndef RAFT_BUILD_BATCH_ID
+#define RAFT_BUILD_BATCH_ID "unknown"
+#endif
+#define RAFT_STR2(x) #x
+#define RAFT_STR(x) RAFT_STR2(x)
+const char* raft_build_batch_source_id(void) {
+    return RAFT_BUILD_BATCH_ID "-t" RAFT_STR(RAFT_TILE_THREADS) "x" RAFT_STR(RAFT_TILE_IPT);
+}
 
 int raft_vote_batch(raft_engine* e, const int64_t* group, const int32_t* dst, const raft_vote_req* req,
                     raft_vote_resp* resp, int64_t n) {

@@ -21,6 +21,7 @@
 #include "../../include/raft_engine.h"
 
 int raft_internal_fail(int code, const std::string& msg);   // raft_engine.hip
+extern "C" int raft_internal_device(const raft_engine* e);   // raft_engine.hip: the engine's GPU
 
 static_assert(RAFT_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "raft_comm ids are ncclUniqueId");
 
@@ -92,11 +93,17 @@ int raft_comm_create(const uint8_t id[RAFT_COMM_ID_BYTES], int32_t nranks, int32
     if (nranks < 1 || rank < 0 || rank >= nranks) return raft_internal_fail(RAFT_EINVAL, "rank outside 0..nranks-1");
     const Rccl& r = rccl();
     if (!r.h) return raft_internal_fail(RAFT_ENODEV, r.err);
+    // ncclCommInitRank binds the communicator to the current device: switch
+    // to `device` for it and give the caller back its own current device
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) return raft_internal_fail(RAFT_EDEVICE, "hipGetDevice failed");
     if (hipSetDevice(device) != hipSuccess) return raft_internal_fail(RAFT_EINVAL, "bad device index");
     ncclUniqueId u;
     std::memcpy(u.internal, id, RAFT_COMM_ID_BYTES);
     ncclComm_t c = nullptr;
-    if (ncclResult_t rc = r.comm_init_rank(&c, nranks, u, rank)) return rccl_fail(r, rc, "ncclCommInitRank");
+    const ncclResult_t rc = r.comm_init_rank(&c, nranks, u, rank);
+    (void)hipSetDevice(prev);
+    if (rc) return rccl_fail(r, rc, "ncclCommInitRank");
     *out = new raft_comm{c, nranks, rank, device};
     return RAFT_OK;
 }
@@ -115,6 +122,9 @@ int raft_engine_allreduce_counters(raft_engine* e, raft_comm* c, const int64_t* 
     if (n_steps == 0) return RAFT_OK;
     const Rccl& r = rccl();
     if (!r.h) return raft_internal_fail(RAFT_ENODEV, r.err);    // (a communicator implies RCCL; defensive)
+    // the all-reduce runs on the engine's stream: the communicator must be on the engine's GPU
+    if (raft_internal_device(e) != c->device)
+        return raft_internal_fail(RAFT_EINVAL, "the communicator and the engine are on different GPUs");
     if (hipSetDevice(c->device) != hipSuccess) return raft_internal_fail(RAFT_EDEVICE, "hipSetDevice failed");
     const size_t count = (size_t)n_steps * RAFT_COUNTER_STRIDE;
     if (ncclResult_t rc = r.all_reduce(counters_dev, out_dev, count, ncclInt64, ncclSum, c->comm,

@@ -557,6 +557,26 @@ __global__ __launch_bounds__(BLOCK) void traffic_probe_kernel(DevParams p, int k
     }
 }
 
+// Scattered-access probes (the handler batches' calibration, include/raft_engine.h
+// RAFT_PROBE_SCATTER_*): thread i touches one 4-byte word at the start of
+// sector s(i) = (i * 2654435761) mod 2^SCATTER_LOG2 of a scratch buffer of
+// 32-byte sectors -- an odd multiplier, so the n < 2^SCATTER_LOG2 sectors are
+// distinct and spread over the whole buffer like a random replica's fields.
+// kind 2 loads (sunk), kind 3 stores; the known traffic is n sectors of 32 B.
+constexpr int SCATTER_LOG2 = 24;                          // 2^24 sectors: a 512 MB scratch
+constexpr int SCATTER_N = 1 << 21;                        // sectors touched per probe
+__global__ __launch_bounds__(BLOCK) void scatter_probe_kernel(uint32_t* scratch, int kind) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t s = (i * 2654435761u) & ((1u << SCATTER_LOG2) - 1u);
+    uint32_t* w = scratch + (size_t)s * 8;
+    if (kind == 2) {
+        const uint32_t v = *w;                                // a plain load, as the handlers' field reads
+        asm volatile("" ::"v"(v));                            // kept: nothing else consumes it
+    } else {
+        *w = i;
+    }
+}
+
 // the retained physical slots of a replica: [max(0, physLen - W), physLen)
 __device__ __forceinline__ int32_t window_lo(const DevParams& p, int32_t phys) { return max(0, phys - p.W); }
 
@@ -976,6 +996,8 @@ template <int R> struct DigestL {
 
 // raft_wire.cpp reports its errors through raft_last_error() too
 int raft_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+// raft_comm.cpp: the engine's GPU (a communicator must be on it)
+extern "C" int raft_internal_device(const raft_engine* e) { return e ? e->device : -1; }
 
 static uint64_t ppm_thr(uint32_t ppm, int bits) {
     // smallest u with u * 1e6 >= ppm << bits  ==  ceil(ppm * 2^bits / 1e6)
@@ -1668,10 +1690,22 @@ int raft_engine_digest_range(raft_engine* e, int64_t g0, int64_t n, uint64_t* ou
 
 int raft_engine_traffic_probe(raft_engine* e, int32_t kind, int64_t* bytes_read, int64_t* bytes_written) {
     if (!e || !bytes_read || !bytes_written) return fail(RAFT_EINVAL, "null argument");
-    if (kind != 0 && kind != 1) return fail(RAFT_EINVAL, "kind must be 0 (state) or 1 (log stores)");
+    if (kind < 0 || kind > 3)
+        return fail(RAFT_EINVAL, "kind must be 0 (state), 1 (log stores), 2 (scattered loads) or 3 (scattered stores)");
     if (kind == 1 && e->p.log_window) return fail(RAFT_EINVAL, "the log-store probe needs a flat log (log_window 0)");
     HIP_TRY(hipSetDevice(e->device));
     e->fork_needed = true;
+    if (kind >= 2) {
+        // engine-owned scratch (the accessors' staging, grow-only): the state is untouched
+        const size_t sz = (size_t)32 << SCATTER_LOG2;
+        if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, sz)) return rc;
+        scatter_probe_kernel<<<SCATTER_N / BLOCK, BLOCK, 0, e->stream>>>((uint32_t*)e->aux, (int)kind);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        *bytes_read = kind == 2 ? (int64_t)SCATTER_N * 32 : 0;
+        *bytes_written = kind == 3 ? (int64_t)SCATTER_N * 32 : 0;
+        return RAFT_OK;
+    }
     if (int rc = grow_dev(e, &e->aux, &e->aux_bytes, 8)) return rc;
     unsigned long long* d = (unsigned long long*)e->aux;
     unsigned long long h = 0;

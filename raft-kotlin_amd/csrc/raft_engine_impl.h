@@ -75,6 +75,7 @@ struct raft_engine {
     // copies of host batches, pinned host staging, pinned status flags
     char* bst;
     size_t bst_bytes;
+    bool bst_dirty;             // the bucketed path's device status words may be nonzero (a batch failed mid-way)
     char* bio;
     size_t bio_bytes;
     char* hst;

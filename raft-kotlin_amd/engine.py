@@ -137,6 +137,12 @@ class RaftEngine:
         """How the handler batches order their messages (abi.BATCH_PATH_AUTO /
         _SORTED / _BUCKETED; results do not depend on it)."""
         self._check(self._lib.raft_engine_set_batch_path(self._h, int(path)), "set_batch_path")
+        self._batch_path = int(path)
+
+    @property
+    def batch_path(self) -> int:
+        """The batch path set with set_batch_path (abi.BATCH_PATH_AUTO unless set)."""
+        return getattr(self, "_batch_path", abi.BATCH_PATH_AUTO)
 
     def reset(self):
         """Every group back to its initial state at step 0 (as created)."""

@@ -1,8 +1,8 @@
 """The handler-batch workload for rocprofv3 (scripts/pmc_handler.sh): bench.py's
 handler_batch leg without the timing loops -- a 10^6 x 5 config-3 engine after
 200 steps, then REPS device-resident batches of N random vote messages and
-REPS of N append messages (bench.handler_requests, seed 12345).  Prints the
-batch plan as JSON for the parser."""
+REPS of N append messages (bench.handler_requests, seed 12345), then the
+scattered-access traffic probes.  Prints the batch plan as JSON for the parser."""
 import importlib
 import json
 import os
@@ -44,10 +44,14 @@ def main():
         for _ in range(REPS):
             fn(d_group.data_ptr(), d_dst.data_ptr(), d_req.data_ptr(), d_resp.data_ptr(), N)
         plan.append([kind, REPS])
+    # the scattered-access calibration (raft_engine_traffic_probe kinds 2 / 3):
+    # known 32-B sectors loaded and stored one word each, in this process's own
+    # --pmc pass, after the batches
+    probes = [[k, *e.traffic_probe(k)] for k in (2, 2, 2, 3, 3, 3)]
     e.close()
     print(json.dumps({"n": N, "batch_path": PATH, "groups": G, "replicas": R, "kernel_src": bench.kernel_source_id(),
-                      "library_src": bench.library_source_id(), "batch_src": bench.batch_source_id(),
-                      "plan": plan}))
+                      "library_src": bench.library_source_id(), "batch_src": abi.build_ids()["batch_source_id"],
+                      "plan": plan, "probes": probes}))
 
 
 if __name__ == "__main__":

@@ -71,8 +71,28 @@ def batches(rows):
         if "batch_keys_kernel" in n or "bucket_tile_kernel" in n:
             cur = []
             out.append(cur)
+        elif "scatter_probe_kernel" in n:                    # the calibration probes end the batches
+            cur = None
         if cur is not None:
             cur.append((n, v))
+    return out
+
+
+def scatter_factors(d, plan):
+    """Bytes per counted byte of scattered single-word accesses: the
+    scatter_probe_kernel dispatches of the same --pmc passes (kind 2 loads in
+    the FETCH_SIZE pass, kind 3 stores in the WRITE_SIZE pass; each moves the
+    32-B sectors the plan states), the median of each kind's dispatches."""
+    probes = plan.get("probes") or []
+    out = {}
+    for c, kind, col in (("FETCH_SIZE", 2, 1), ("WRITE_SIZE", 3, 2)):
+        known = [p[col] for p in probes if p[0] == kind]
+        rows = [v for _, nm, v in kernels(f"{d}/pmc_{c}", c) if "scatter_probe_kernel" in nm]
+        vals = rows[:3] if kind == 2 else rows[3:]
+        if not known or not vals:
+            return None
+        r = sorted(known[i] / (v * 1024.0) for i, v in enumerate(vals[: len(known)]) if v)
+        out[c] = {"factor": r[len(r) // 2], "probe_kb_raw": sorted(vals), "probe_bytes": known[0]}
     return out
 
 
@@ -81,7 +101,11 @@ def main(d):
     state = CALIB_G * (CALIB_R * REPLICA_BYTES + GROUP_BYTES)
     cf = sorted(pmc_parse.dispatches(f"{d}/calib_FETCH_SIZE").get("FETCH_SIZE", []))
     cw = sorted(pmc_parse.dispatches(f"{d}/calib_WRITE_SIZE").get("WRITE_SIZE", []))
-    ff, wf = state / (cf[len(cf) // 2] * 1024.0), state / (cw[len(cw) // 2] * 1024.0)
+    # streaming factors (the calibration engine's state launches) and, when the
+    # probe ran, the scattered-access factors that the handler rows use
+    sff, swf = state / (cf[len(cf) // 2] * 1024.0), state / (cw[len(cw) // 2] * 1024.0)
+    sc = scatter_factors(d, plan)
+    ff, wf = (sc["FETCH_SIZE"]["factor"], sc["WRITE_SIZE"]["factor"]) if sc else (sff, swf)
     fb, wb, tb = (batches(kernels(f"{d}/pmc_FETCH_SIZE", "FETCH_SIZE")),
                   batches(kernels(f"{d}/pmc_WRITE_SIZE", "WRITE_SIZE")), batches(kernels(f"{d}/trace")))
     kinds = [k for k, reps in plan["plan"] for _ in range(reps)]
@@ -95,7 +119,8 @@ def main(d):
         def avg(bl, sel=lambda nm: True):
             return sum(sum(v for nm, v in bl[i] if sel(nm)) for i in ix) / len(ix)
         hk = lambda nm: "batch_kernel" in nm  # noqa: E731
-        fetch, write = avg(fb) * 1024 * ff, avg(wb) * 1024 * wf
+        fkb, wkb = avg(fb), avg(wb)                         # raw FETCH_SIZE / WRITE_SIZE, KB per batch
+        fetch, write = fkb * 1024 * ff, wkb * 1024 * wf
         hfetch, hwrite = avg(fb, hk) * 1024 * ff, avg(wb, hk) * 1024 * wf
         t_all, t_h = avg(tb) / 1e6, avg(tb, hk) / 1e6
         rows.append({"kind": kind, "n": n, "groups": plan["groups"], "replicas": plan["replicas"],
@@ -109,7 +134,12 @@ def main(d):
                      "kernels_ms_per_batch": t_all, "handler_kernel_ms": t_h,
                      "handler_kernel_hbm_gbs": (hfetch + hwrite) / (t_h / 1e3) / 1e9 if t_h else None,
                      "kernels_per_batch": runs([short(nm) for nm, _ in tb[ix[0]]]),
+                     "fetch_kb_raw": fkb, "write_kb_raw": wkb,
+                     "raw_bytes_per_message": (fkb + wkb) * 1024 / n,
+                     "streaming_calibrated_bytes_per_message": (fkb * sff + wkb * swf) * 1024 / n,
                      "fetch_factor": ff, "write_factor": wf,
+                     "calibration": "scatter" if sc else "streaming",
+                     "scatter_probe": sc, "streaming_factors": {"fetch": sff, "write": swf},
                      "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes + --kernel-trace "
                                f"(scripts/pmc_handler.sh, {os.path.basename(d)})"})
     json.dump(rows, open(os.path.join(d, "handler_rows.json"), "w"), indent=1)
@@ -121,7 +151,7 @@ def merge(files):
         have = json.load(open(OUT_FILE))
     except (OSError, ValueError):
         have = []
-    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"],  # noqa: E731
+    key = lambda r: (r["kind"], r["n"], r["groups"], r["replicas"], r.get("batch_path", 0),  # noqa: E731
                      r.get("batch_src") or r.get("library_src") or r["kernel_src"])
     out = {key(r): r for r in have}
     for f in files:

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-6 GPU sessions, one named preset per call:
+#   gpurun -- 'PRESET=a bash scripts/sessions/r6.sh'
+# Every GPU step has its own time limit and a failure ends the script.
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+P=${PRESET:?set PRESET}
+OUT=gpurun_out/r6_$P${TAGS:-}; mkdir -p "$OUT"
+step() {   # step NAME LIMIT CMD...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/status.txt"
+  [ $rc -eq 0 ] || [ $rc -eq 1 -a "$name" = pytest ] || exit $rc
+}
+summ() {   # one line per log: value, wall, kernel, all-reduce
+  for f in "$@"; do
+    echo "$(basename $f) $(grep -o '"value": [0-9.e+]*' $f | head -1) $(grep -o '"wall_ms": [0-9.]*' $f | head -1) $(grep -o '"kernel_avg_ms": [0-9.]*' $f | head -1) $(grep -o '"allreduce_ms": [0-9.enul]*' $f | head -1)"
+  done
+}
+Q="--no-cpu-baseline --handler-batch 0 --no-general-leg --stream-steps 0"
+case $P in
+  a)  # VALU issue cost per instruction class (scripts/ubench/valu_rate4.hip); the short shard's host-side
+      # A/B (kernel timestamps on the launches; polling the last event before the closing sync), with the
+      # one-rank native all-reduce inside the clock; the handler batches' scattered-access calibration
+      step ubench4 120 ./scripts/ubench/valu_rate4
+      for i in 1 2; do
+        for ev in 1 0; do
+          for sy in block spin; do
+            tag=s8_ev${ev}_${sy}_$i
+            RAFT_BENCH_NO_KERNEL_EVENTS=$([ $ev = 0 ] && echo 1 || echo 0) RAFT_BENCH_FORCE_COLLECTIVE=1 \
+              step $tag 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 --sync $sy $Q
+          done
+        done
+        step d20_block_$i 200 python -u bench.py --steps 20 --warmup 5 --sync block $Q
+        step d20_spin_$i 200 python -u bench.py --steps 20 --warmup 5 --sync spin $Q
+      done
+      summ $OUT/s8_*.log $OUT/d20_*.log > $OUT/summary.txt
+      TAG=r6_a step pmch 900 bash scripts/pmc_handler.sh
+      ;;
+  *) echo "unknown preset $P"; exit 2 ;;
+esac
+exit 0
