@@ -55,9 +55,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS, CLOCK_HZ, VALU_CYCLES = 1024, 2.4e9, 2
 VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 # per replica: 10 canonical fields + the log-tail cache (t1, t2, c1) + the
-# primary-session column (nextIndex, matchIndex); per group: 3 harness words
-REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
-GROUP_BYTES = 4 * 3
+# primary-session column (nextIndex, matchIndex) in 4 int32 quads; per group: 3 harness words
+REPLICA_BYTES, GROUP_BYTES = abi.REPLICA_STATE_BYTES, abi.GROUP_STATE_BYTES
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
 SCHEDULES = {"auto": abi.SCHED_AUTO, "one": abi.SCHED_ONE_PER_WAVE, "balanced": abi.SCHED_BALANCED}
 

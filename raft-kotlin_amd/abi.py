@@ -96,6 +96,10 @@ C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
 FIELD_NAMES = ["term", "voted", "role", "commit", "last", "phys",
                "election_ms", "flags", "phase_ms", "retry_ms"]
 NUM_FIELDS = len(FIELD_NAMES)
+# the engine's HBM state per replica: 4 quads of int32 (the 10 fields, the
+# log-tail cache and the primary session column; raft_step.h FIELD_SLOT), and
+# per group: 3 harness words
+REPLICA_STATE_BYTES, GROUP_STATE_BYTES = 64, 12
 F_INDEX = {n: i for i, n in enumerate(FIELD_NAMES)}
 FL_ARMED, FL_ELECTING, FL_PENDING_RST, FL_HB_ACTIVE, FL_BACKOFF = 1, 2, 4, 8, 16
 GROUP_EXTRA = 2

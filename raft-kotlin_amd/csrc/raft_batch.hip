@@ -49,47 +49,40 @@ struct RepState {
     __device__ Rep ref() { return Rep{term, voted, role, commit, last, phys, elec, phase, retry, fl, t1, t2, c1}; }
 };
 
-// VOTE_ONLY: the fields vote() and the timer re-arm touch (RaftServer.kt:228-251)
-// -- the others are neither read nor written back
+// The replica's state quads a handler needs (raft_step.h FIELD_SLOT), one
+// 16-B access and one 32-B sector each: quad 0 (term, votedFor, state, flags)
+// and quad 1 (lastIndex, physLen, t1, electionMs) for vote() and the timer
+// re-arm (RaftServer.kt:228-251); quad 2 (commitIndex, t2, c1, phaseMs) too
+// for append() and appendCommand (:253-287, :100-107).  Quad 3 (retryMs and
+// the primary session) no handler touches.  The log-tail cache (t1, t2, c1)
+// is the HBM copy: the batch path keeps it valid (run_batch_dev rebuilds it
+// first when a host write left it stale, and every run stores it back), so
+// vote() reads no log slot at all.
+struct RepQuads {
+    int4 q0, q1, q2;
+};
 template <bool VOTE_ONLY = false>
-__device__ __forceinline__ void load_rep(RepState& x, const DevParams& p, int64_t idx) {
-#define LD(f) p.st[fidx(p, f, idx)]
-    x.term = LD(RAFT_F_TERM); x.voted = LD(RAFT_F_VOTED); x.role = LD(RAFT_F_ROLE);
-    x.last = LD(RAFT_F_LAST); x.phys = LD(RAFT_F_PHYS); x.fl = (uint32_t)LD(RAFT_F_FLAGS);
-    if (VOTE_ONLY) {
-        x.commit = x.elec = x.phase = x.retry = 0;
-    } else {
-        x.commit = LD(RAFT_F_COMMIT); x.elec = LD(RAFT_F_ELECTION_MS);
-        x.phase = LD(RAFT_F_PHASE_MS); x.retry = LD(RAFT_F_RETRY_MS);
-    }
-#undef LD
+__device__ __forceinline__ void load_rep(RepState& x, RepQuads& o, const DevParams& p, int64_t idx) {
+    o.q0 = *quad(p, 0, idx);
+    o.q1 = *quad(p, 1, idx);
+    o.q2 = VOTE_ONLY ? make_int4(0, 0, 0, 0) : *quad(p, 2, idx);
+    x.term = o.q0.x; x.voted = o.q0.y; x.role = o.q0.z; x.fl = (uint32_t)o.q0.w;
+    x.last = o.q1.x; x.phys = o.q1.y; x.t1 = o.q1.z; x.elec = o.q1.w;
+    x.commit = o.q2.x; x.t2 = o.q2.y; x.c1 = (uint32_t)o.q2.z; x.phase = o.q2.w;
+    x.retry = 0;                                                        // (quad 3: no handler touches it)
 }
 
-// the batch path derives the tail cache from the log (the HBM copy may be
-// stale); vote() reads only the last entry's term
+// Only the quads that changed are written back, whole (the run's thread owns
+// the replica): a random replica's quad is a 32-B sector of its own.
 template <bool VOTE_ONLY = false>
-__device__ __forceinline__ void derive_cache(RepState& x, const LogView& lv) {
-    const uint2 a = x.last >= 1 ? *lv.at(x.last - 1) : make_uint2(0u, 0u);
-    x.t1 = (int32_t)a.x;
-    x.c1 = a.y;
-    x.t2 = !VOTE_ONLY && x.last >= 2 ? (int32_t)lv.at(x.last - 2)->x : 0;
-}
-
-// Only the fields that changed are written back: a random replica's field is
-// a 32-B sector of its own, so an unchanged field would cost a sector write.
-// drew: the timer was re-armed (resolve_rep_draw wrote elec).
-template <bool VOTE_ONLY = false>
-__device__ __forceinline__ void store_rep(const RepState& x, const RepState& o, bool drew, const DevParams& p,
-                                          int64_t idx) {
-#define ST(f, v, w) if ((v) != (w)) p.st[fidx(p, f, idx)] = (v)
-    ST(RAFT_F_TERM, x.term, o.term); ST(RAFT_F_VOTED, x.voted, o.voted); ST(RAFT_F_ROLE, x.role, o.role);
-    ST(RAFT_F_FLAGS, (int32_t)(x.fl & FL_EXPORT_MASK), (int32_t)(o.fl & FL_EXPORT_MASK));
-    if (drew || (!VOTE_ONLY && x.elec != o.elec)) p.st[fidx(p, RAFT_F_ELECTION_MS, idx)] = x.elec;
-    if (!VOTE_ONLY) {
-        ST(RAFT_F_COMMIT, x.commit, o.commit); ST(RAFT_F_LAST, x.last, o.last); ST(RAFT_F_PHYS, x.phys, o.phys);
-        ST(RAFT_F_PHASE_MS, x.phase, o.phase); ST(RAFT_F_RETRY_MS, x.retry, o.retry);
-    }
-#undef ST
+__device__ __forceinline__ void store_rep(const RepState& x, const RepQuads& o, const DevParams& p, int64_t idx) {
+    const int4 q0 = make_int4(x.term, x.voted, x.role, (int32_t)(x.fl & FL_EXPORT_MASK));
+    const int4 q1 = make_int4(x.last, x.phys, x.t1, x.elec);
+    const int4 q2 = make_int4(x.commit, x.t2, (int32_t)x.c1, x.phase);
+    auto differ = [](int4 a, int4 b) { return a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w; };
+    if (differ(q0, o.q0)) *quad(p, 0, idx) = q0;
+    if (differ(q1, o.q1)) *quad(p, 1, idx) = q1;
+    if (!VOTE_ONLY && differ(q2, o.q2)) *quad(p, 2, idx) = q2;
 }
 
 __device__ __forceinline__ bool resolve_rep_draw(RepState& x, const DevParams& p, uint32_t t, uint32_t gid, int r) {
@@ -158,12 +151,10 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
     uint32_t om = ord(m0);
     Req q = ((const Req*)req)[om];
     RepState x;
-    load_rep<VO>(x, p, idx);
-    const RepState o = x;
+    RepQuads o;
+    load_rep<VO>(x, o, p, idx);
     const LogView lv = log_of(p, idx);
-    derive_cache<VO>(x, lv);
     BatchCounters cnt;
-    bool drew = false;
     for (int m = m0;;) {
         const Req qm = q;
         const uint32_t oc = om;
@@ -182,8 +173,12 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
             int32_t rt = 0;
             uint64_t su = 0, st = 0;
             const int32_t pv = qm.prev_log_index;
-            const int32_t dprev = (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
-            const int32_t dnext = (TB && pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
+            // log[prev] (and TB: log[prev + 1]) from the tail cache when it
+            // holds them, else from the log
+            const int32_t dprev = pv == x.last - 1 ? x.t1 : pv == x.last - 2 ? x.t2
+                                  : (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
+            const int32_t dnext = !TB ? 0 : pv + 1 == x.last - 1 ? x.t1 : pv + 1 == x.last - 2 ? x.t2
+                                  : (pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
             const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, qm.term, qm.leader_id,
                                                        pv, qm.prev_log_term, __ballot(qm.has_entry != 0),
                                                        Entry{qm.entry_term, qm.entry_cmd}, qm.leader_commit, dprev,
@@ -194,10 +189,10 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
         } else {
             append_command<TB, true>(x.ref(), __ballot(1), lv, qm, cnt);
         }
-        drew |= resolve_rep_draw(x, p, t, gid, r);
+        resolve_rep_draw(x, p, t, gid, r);
         if (!more(++m)) break;
     }
-    store_rep<VO>(x, o, drew, p, idx);
+    store_rep<VO>(x, o, p, idx);
     if (cnt.miss) {
         atomicAdd(&flags[1], cnt.miss);
         if (hmiss) *(volatile unsigned int*)hmiss = 1u;                 // (bucket path: the host copies the count)
@@ -571,6 +566,9 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
 static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const int32_t* dst, const void* req,
                          void* resp, int64_t n64) {
     e->fork_needed = true;
+    // the handlers read and write the HBM tail cache: rebuilt first if a host
+    // write left it stale (then it stays valid: the batches keep it)
+    raft_internal_ensure_cache(e);
     const int n = (int)n64;
     const uint64_t nkeys = (uint64_t)e->p.G * (uint64_t)e->p.R;
     int bits = 1;
@@ -582,7 +580,6 @@ static int run_batch_dev(raft_engine* e, int kind, const int64_t* group, const i
                    : bits <= 32 ? run_batch_keys<uint32_t>(e, kind, group, dst, req, resp, n, bits)
                                 : run_batch_keys<uint64_t>(e, kind, group, dst, req, resp, n, bits);
     if (rc) return rc;
-    e->cache_valid = false;
     if (e->bflags_host[0]) return fail(RAFT_ERANGE, "a message's group or replica index is outside the engine; "
                                                     "nothing was applied");
     if (e->bflags_host[1])

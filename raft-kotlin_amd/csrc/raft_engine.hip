@@ -70,26 +70,31 @@ static_assert(STEP_K_7WG >= 400, "bench.py's launch length (abi.BENCH_STEPS_PER_
 // ---------------------------------------------------------------------------
 // replica state <-> registers
 // ---------------------------------------------------------------------------
+// (the quads' word order: raft_step.h FIELD_SLOT).  One dword access per
+// field: merged into dwordx4 per quad, the accesses need 4 consecutive VGPRs
+// each, and the step kernel's register allocation spilled 60 B to scratch to
+// find them (the compiler barriers keep the loads in flight together)
+#define NOMERGE asm volatile("" ::: "memory")
 __device__ __forceinline__ void load_node(Node& n, const DevParams& p, int64_t g, int64_t idx) {
     const int32_t* st = p.st;
-    n.term = st[fidx(p, RAFT_F_TERM, idx)];
-    n.voted = st[fidx(p, RAFT_F_VOTED, idx)];
-    n.role = st[fidx(p, RAFT_F_ROLE, idx)];
-    n.commit = st[fidx(p, RAFT_F_COMMIT, idx)];
-    n.last = st[fidx(p, RAFT_F_LAST, idx)];
-    n.phys = st[fidx(p, RAFT_F_PHYS, idx)];
-    n.elec = st[fidx(p, RAFT_F_ELECTION_MS, idx)];
-    n.fl = (uint32_t)st[fidx(p, RAFT_F_FLAGS, idx)];
-    n.phase = st[fidx(p, RAFT_F_PHASE_MS, idx)];
-    n.retry = st[fidx(p, RAFT_F_RETRY_MS, idx)];
-    n.t1 = st[fidx(p, F_T1, idx)];
-    n.t2 = st[fidx(p, F_T2, idx)];
-    n.c1 = (uint32_t)st[fidx(p, F_C1, idx)];
-    n.nx = p.ses[idx];
-    n.mc = p.ses[p.GR + idx];
-    n.iso = p.gx[GX_ISO * p.G + g];
-    n.cmdc = p.gx[GX_CMDS * p.G + g];
-    n.s0 = p.gx[GX_S0 * p.G + g];
+    NOMERGE; n.term = st[fidx(p, RAFT_F_TERM, idx)];
+    NOMERGE; n.voted = st[fidx(p, RAFT_F_VOTED, idx)];
+    NOMERGE; n.role = st[fidx(p, RAFT_F_ROLE, idx)];
+    NOMERGE; n.commit = st[fidx(p, RAFT_F_COMMIT, idx)];
+    NOMERGE; n.last = st[fidx(p, RAFT_F_LAST, idx)];
+    NOMERGE; n.phys = st[fidx(p, RAFT_F_PHYS, idx)];
+    NOMERGE; n.elec = st[fidx(p, RAFT_F_ELECTION_MS, idx)];
+    NOMERGE; n.fl = (uint32_t)st[fidx(p, RAFT_F_FLAGS, idx)];
+    NOMERGE; n.phase = st[fidx(p, RAFT_F_PHASE_MS, idx)];
+    NOMERGE; n.retry = st[fidx(p, RAFT_F_RETRY_MS, idx)];
+    NOMERGE; n.t1 = st[fidx(p, F_T1, idx)];
+    NOMERGE; n.t2 = st[fidx(p, F_T2, idx)];
+    NOMERGE; n.c1 = (uint32_t)st[fidx(p, F_C1, idx)];
+    NOMERGE; n.nx = st[fidx(p, F_NX, idx)];
+    NOMERGE; n.mc = st[fidx(p, F_MC, idx)];
+    NOMERGE; n.iso = p.gx[GX_ISO * p.G + g];
+    NOMERGE; n.cmdc = p.gx[GX_CMDS * p.G + g];
+    NOMERGE; n.s0 = p.gx[GX_S0 * p.G + g];
 }
 
 __device__ __forceinline__ void inert_node(Node& n) {
@@ -106,21 +111,21 @@ __device__ __forceinline__ void inert_node(Node& n) {
 
 __device__ __forceinline__ void store_node(const Node& n, const DevParams& p, int64_t g, int64_t idx, bool group_lead) {
     int32_t* st = p.st;
-    st[fidx(p, RAFT_F_TERM, idx)] = n.term;
-    st[fidx(p, RAFT_F_VOTED, idx)] = n.voted;
-    st[fidx(p, RAFT_F_ROLE, idx)] = n.role;
-    st[fidx(p, RAFT_F_COMMIT, idx)] = n.commit;
-    st[fidx(p, RAFT_F_LAST, idx)] = n.last;
-    st[fidx(p, RAFT_F_PHYS, idx)] = n.phys;
-    st[fidx(p, RAFT_F_ELECTION_MS, idx)] = n.elec;
-    st[fidx(p, RAFT_F_FLAGS, idx)] = (int32_t)(n.fl & FL_EXPORT_MASK);
-    st[fidx(p, RAFT_F_PHASE_MS, idx)] = n.phase;
-    st[fidx(p, RAFT_F_RETRY_MS, idx)] = n.retry;
-    st[fidx(p, F_T1, idx)] = n.t1;
-    st[fidx(p, F_T2, idx)] = n.t2;
-    st[fidx(p, F_C1, idx)] = (int32_t)n.c1;
-    p.ses[idx] = n.nx;
-    p.ses[p.GR + idx] = n.mc;
+    NOMERGE; st[fidx(p, RAFT_F_TERM, idx)] = n.term;
+    NOMERGE; st[fidx(p, RAFT_F_VOTED, idx)] = n.voted;
+    NOMERGE; st[fidx(p, RAFT_F_ROLE, idx)] = n.role;
+    NOMERGE; st[fidx(p, RAFT_F_COMMIT, idx)] = n.commit;
+    NOMERGE; st[fidx(p, RAFT_F_LAST, idx)] = n.last;
+    NOMERGE; st[fidx(p, RAFT_F_PHYS, idx)] = n.phys;
+    NOMERGE; st[fidx(p, RAFT_F_ELECTION_MS, idx)] = n.elec;
+    NOMERGE; st[fidx(p, RAFT_F_FLAGS, idx)] = (int32_t)(n.fl & FL_EXPORT_MASK);
+    NOMERGE; st[fidx(p, RAFT_F_PHASE_MS, idx)] = n.phase;
+    NOMERGE; st[fidx(p, RAFT_F_RETRY_MS, idx)] = n.retry;
+    NOMERGE; st[fidx(p, F_T1, idx)] = n.t1;
+    NOMERGE; st[fidx(p, F_T2, idx)] = n.t2;
+    NOMERGE; st[fidx(p, F_C1, idx)] = (int32_t)n.c1;
+    NOMERGE; st[fidx(p, F_NX, idx)] = n.nx;
+    NOMERGE; st[fidx(p, F_MC, idx)] = n.mc;
     if (group_lead) {
         p.gx[GX_ISO * p.G + g] = n.iso;
         p.gx[GX_CMDS * p.G + g] = n.cmdc;
@@ -128,14 +133,15 @@ __device__ __forceinline__ void store_node(const Node& n, const DevParams& p, in
     }
 }
 
-// canonical session rows: the primary (owner s0) lives in ses, the rest in spill
+// canonical session rows: the primary (owner s0) lives in the state quads
+// (F_NX / F_MC), the rest in spill
 __device__ __forceinline__ int32_t canon_next(const DevParams& p, int R, int64_t g, int s0, int s, int d) {
     const int64_t idx = g * R + d;
-    return s == s0 ? p.ses[idx] : p.spill[idx * R + s];
+    return s == s0 ? p.st[fidx(p, F_NX, idx)] : p.spill[idx * R + s];
 }
 __device__ __forceinline__ int32_t canon_match(const DevParams& p, int R, int64_t g, int s0, int s, int d) {
     const int64_t idx = g * R + d;
-    return s == s0 ? p.ses[p.GR + idx] : p.spill[p.GR * R + idx * R + s];
+    return s == s0 ? p.st[fidx(p, F_MC, idx)] : p.spill[p.GR * R + idx * R + s];
 }
 
 // ---------------------------------------------------------------------------
@@ -150,13 +156,11 @@ __global__ __launch_bounds__(BLOCK) void init_kernel(DevParams p) {
     const int64_t g = idx / R;
     const int r = (int)(idx - g * R);
     const uint32_t gid = (uint32_t)(p.g0 + g);
-    for (int f = 0; f < F_DEV; ++f) p.st[fidx(p, f, idx)] = 0;
+    for (int q = 0; q < ST_QUADS; ++q) *quad(p, q, idx) = make_int4(0, 0, 0, 0);   // sessions and tail cache too
     p.st[fidx(p, RAFT_F_VOTED, idx)] = -1;                               // RaftServer.kt:39
     const u32x4 w = draw(p, RAFT_RNG_INIT_STEP, gid, RAFT_RNG_TIMER, (uint32_t)(r >> 2));
     p.st[fidx(p, RAFT_F_ELECTION_MS, idx)] = scale_range(word_of(w, r & 3), p.emin, p.emax);
     p.st[fidx(p, RAFT_F_FLAGS, idx)] = (int32_t)FL_ARMED;
-    p.ses[idx] = 0;
-    p.ses[p.GR + idx] = 0;
     for (int s = 0; s < R; ++s) {
         p.spill[idx * R + s] = 0;
         p.spill[p.GR * R + idx * R + s] = 0;
@@ -334,7 +338,7 @@ __device__ __forceinline__ void enter_piece(Ctx<R>& c, Node& n, int wid) {
     using L = Lanes<R>;
     const KernArgs kp = kernargs();
     DevParams p;
-    p.st = kp->st; p.ses = kp->ses; p.gx = kp->gx; p.GR = kp->GR; p.G = kp->G;
+    p.st = kp->st; p.gx = kp->gx; p.GR = kp->GR; p.G = kp->G;
     const int j = (int)c.j();
     const int64_t g = (int64_t)wid * L::GPW + j;
     c.live = j < L::GPW && g < p.G;
@@ -466,7 +470,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             if (c.live) {
                 const KernArgs kp = kernargs();    // state pointers re-read, not kept live across the loop
                 DevParams q;
-                q.st = kp->st; q.ses = kp->ses; q.gx = kp->gx; q.GR = kp->GR; q.G = kp->G;
+                q.st = kp->st; q.gx = kp->gx; q.GR = kp->GR; q.G = kp->G;
                 store_node(n, q, (int64_t)c.wg0 + j, c.idx(), r == 0);
             }
             // this wave's index from its job rows' address (kept live across
@@ -525,7 +529,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
 // byte count, in the same process and on the same box as the launches they
 // calibrate.  One wave per chunk, the step kernel's lane geometry.
 //  kind 0: each chunk's state into VGPRs and back, exactly as a piece's entry
-//          and exit (load_node / store_node): G * (R * 60 + 12) bytes read and
+//          and exit (load_node / store_node): G * (R * 64 + 12) bytes read and
 //          the same written, values unchanged.
 //  kind 1: one 8-byte store per replica into its own log row at slot physLen
 //          (a flat log's slot past the last entry, never read), the pattern of
@@ -996,6 +1000,12 @@ template <int R> struct DigestL {
 
 // raft_wire.cpp reports its errors through raft_last_error() too
 int raft_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+void raft_internal_ensure_cache(raft_engine* e) {
+    if (e->cache_valid) return;
+    rebuild_cache_kernel<<<(unsigned)((e->dp.GR + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp);
+    e->cache_valid = true;
+    e->fork_needed = true;
+}
 // raft_comm.cpp: the engine's GPU (a communicator must be on it)
 extern "C" int raft_internal_device(const raft_engine* e) { return e ? e->device : -1; }
 
@@ -1128,8 +1138,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     d.GR = G * R;
     e->K = p->steps_per_launch > 0 ? p->steps_per_launch : 1;
 
-    const size_t st_b = (size_t)F_DEV * R * G * 4;
-    const size_t ses_b = (size_t)2 * R * G * 4;
+    const size_t st_b = (size_t)ST_QUADS * 16 * R * G;
     const size_t spill_b = (size_t)2 * R * R * G * 4;
     const size_t gx_b = (size_t)GX_WORDS * G * 4;
     const size_t log_b = (size_t)log_waves * nslots * 64 * 8;
@@ -1138,7 +1147,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;
     const size_t cnt_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * RAFT_COUNTER_STRIDE * 8;
     const size_t acc_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NC * 8;
-    e->bytes = al(st_b) + al(ses_b) + al(spill_b) + al(gx_b) + 2 * al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
+    e->bytes = al(st_b) + al(spill_b) + al(gx_b) + 2 * al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
     hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (err != hipSuccess) { delete e; return fail(RAFT_EDEVICE, "hipStreamCreate failed"); }
     err = hipMalloc(&e->base, e->bytes);
@@ -1149,7 +1158,6 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     }
     char* b = (char*)e->base;
     d.st = (int32_t*)b; b += al(st_b);
-    d.ses = (int32_t*)b; b += al(ses_b);
     d.spill = (int32_t*)b; b += al(spill_b);
     d.gx = (int32_t*)b; b += al(gx_b);
     e->partials = (uint32_t*)b; b += al(part_b);
@@ -1273,11 +1281,7 @@ static int reserve_events(raft_engine* e, size_t pairs) {
 int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_dev) {
     if (!e || n_steps < 0) return fail(RAFT_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(e->device));
-    if (!e->cache_valid && n_steps > 0) {
-        rebuild_cache_kernel<<<(unsigned)((e->dp.GR + BLOCK - 1) / BLOCK), BLOCK, 0, e->stream>>>(e->dp);
-        e->cache_valid = true;
-        e->fork_needed = true;
-    }
+    if (n_steps > 0) raft_internal_ensure_cache(e);
     // One sub-range: every launch and its counter reduction on the engine
     // stream.  nsub > 1: launch k of sub-range q runs on sub_stream[q] and
     // writes its workgroups' columns of partials buffer k & 1; the engine
@@ -1717,7 +1721,7 @@ int raft_engine_traffic_probe(raft_engine* e, int32_t kind, int64_t* bytes_read,
     if (err == hipSuccess) err = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, e->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     if (err != hipSuccess) return fail(RAFT_EDEVICE, hipGetErrorString(err));
-    const int64_t state = e->p.G * ((int64_t)e->p.R * (4 * F_DEV + 8) + 4 * GX_WORDS);
+    const int64_t state = e->p.G * ((int64_t)e->p.R * 16 * ST_QUADS + 4 * GX_WORDS);
     *bytes_read = kind == 0 ? state : 4 * e->p.G * e->p.R;               // kind 1 reads physLen
     *bytes_written = kind == 0 ? state : 8 * (int64_t)h;
     return RAFT_OK;

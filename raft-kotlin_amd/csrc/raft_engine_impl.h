@@ -17,6 +17,9 @@ using namespace raft;
 int raft_internal_fail(int code, const std::string& msg);
 extern "C" int raft_internal_grow_dev(raft_engine* e, char** buf, size_t* have, size_t need);
 extern "C" int raft_internal_grow_host(raft_engine* e, char** buf, size_t* have, size_t need);
+// raft_engine.hip: enqueue the log-tail cache's rebuild on the engine stream
+// if a host write left it stale (cache_valid false)
+void raft_internal_ensure_cache(raft_engine* e);
 
 namespace {
 
@@ -25,8 +28,16 @@ constexpr int WAVES_PER_BLOCK = BLOCK / 64;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// field f of replica idx = g * R + r in the state arrays (DevParams::st)
-__device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) { return (int64_t)f * p.GR + idx; }
+// field f of replica idx = g * R + r in the state quads (DevParams::st,
+// raft_step.h FIELD_SLOT): word f & 3 of quad f >> 2 of the replica's slots
+__device__ __forceinline__ int64_t fidx(const DevParams& p, int f, int64_t idx) {
+    const int s = FIELD_SLOT[f];
+    return ((int64_t)(s >> 2) * p.GR + idx) * 4 + (s & 3);
+}
+// quad q of replica idx (16-B aligned: the state array starts on 256 B)
+__device__ __forceinline__ int4* quad(const DevParams& p, int q, int64_t idx) {
+    return (int4*)p.st + (int64_t)q * p.GR + idx;
+}
 
 // the log of replica idx = g * R + r outside the step kernel: lane
 // (g % GPW) * R + r of the block of step-kernel wave g / GPW
@@ -87,7 +98,8 @@ struct raft_engine {
     int64_t* counters_dev;      // [K][STRIDE] scratch
     unsigned long long* accum;  // [K * NC] counter accumulators: sum + chunks done << 48 (zero between launches)
     // step-kernel event timing
-    bool cache_valid;           // log-tail cache in st[F_T1..F_C1] matches state + logs
+    bool cache_valid;           // log-tail cache (F_T1, F_T2, F_C1) matches state + logs: the step kernel and the
+                                // handler batches keep it; write_state / write_log make it stale
     bool iso_written;           // write_state stored a nonzero isolation word (step_fn: NET_ISO kernels)
     bool timing;
     std::vector<hipEvent_t> ev;  // pool, pairs (one per sub-range launch)

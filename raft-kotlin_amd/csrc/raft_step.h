@@ -83,16 +83,33 @@ constexpr uint32_t FL_EXPORT_MASK = ~FL_DRAW;
 constexpr int PEND_SH = RAFT_FL_PENDING_SHIFT, VOTES_SH = RAFT_FL_VOTES_SHIFT, LATCH_SH = RAFT_FL_LATCH_SHIFT;
 
 // engine-internal per-replica fields after the canonical ones: the log-tail
-// cache (term of log[last-1], log[last-2]; cmd of log[last-1])
+// cache (term of log[last-1], log[last-2]; cmd of log[last-1]) and the
+// group's primary leader session towards this replica (nextIndex, matchIndex)
 constexpr int F_T1 = RAFT_NUM_FIELDS, F_T2 = RAFT_NUM_FIELDS + 1, F_C1 = RAFT_NUM_FIELDS + 2;
-constexpr int F_DEV = RAFT_NUM_FIELDS + 3;
+constexpr int F_NX = RAFT_NUM_FIELDS + 3, F_MC = RAFT_NUM_FIELDS + 4;
+constexpr int F_DEV = RAFT_NUM_FIELDS + 5;
+// The 15 fields live in 4 quads of 4 int32 per replica (st, below): a piece
+// entry / exit moves a replica with 4 dwordx4 accesses, and a handler of the
+// batch path touches only the quads it needs, one 32-B sector each (vote():
+// quads 0 and 1, append(): 0-2).  Slot 4q + k of a field = word k of quad q.
+//   quad 0: term, votedFor, state, flags       (every handler reads and writes)
+//   quad 1: lastIndex, physLen, t1, electionMs (vote() reads, the timer re-arm writes)
+//   quad 2: commitIndex, t2, c1, phaseMs       (append() and appendCommand)
+//   quad 3: retryMs, nextIndex, matchIndex, -  (the step kernel only)
+constexpr int ST_QUADS = 4;
+constexpr int FIELD_SLOT[F_DEV] = {
+    /* TERM */ 0, /* VOTED */ 1, /* ROLE */ 2, /* COMMIT */ 8, /* LAST */ 4, /* PHYS */ 5,
+    /* ELECTION_MS */ 7, /* FLAGS */ 3, /* PHASE_MS */ 11, /* RETRY_MS */ 12,
+    /* T1 */ 6, /* T2 */ 9, /* C1 */ 10, /* NX */ 13, /* MC */ 14,
+};
+static_assert(RAFT_NUM_FIELDS == 10 && RAFT_F_RETRY_MS == 9, "FIELD_SLOT lists the canonical fields in order");
 // group words gx[GX_*][G]
 constexpr int GX_ISO = 0, GX_CMDS = 1, GX_S0 = 2, GX_WORDS = 3;
 
 // HBM layout (all per-replica arrays indexed by idx = g * R + r, so the lanes
-// of a wave read one contiguous run per field):
-//   st    int32 [F_DEV][G*R]        replica scalars + tail cache
-//   ses   int32 [2][G*R]            primary session of group g: nextIndex / matchIndex towards replica r
+// of a wave read one contiguous run per quad):
+//   st    int4  [ST_QUADS][G*R]     replica scalars, tail cache and the primary session of group g
+//                                   (nextIndex / matchIndex towards replica r), FIELD_SLOT
 //   spill int32 [2][G*R][R]         every other session row: [(g*R + d) * R + s]
 //   gx    int32 [GX_WORDS][G]       isolation word, commands issued, primary-session owner s0 (-1 none)
 //   log   uint2 [waves][64][NW]     (term, cmd) physical slots, one contiguous block per step-kernel
@@ -101,7 +118,6 @@ constexpr int GX_ISO = 0, GX_CMDS = 1, GX_S0 = 2, GX_WORDS = 3;
 //                                   of the newest NW slots) or log_cap (every slot, no wrap)
 struct DevParams {
     int32_t* st;
-    int32_t* ses;
     int32_t* spill;
     int32_t* gx;
     uint2* log;

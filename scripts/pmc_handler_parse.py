@@ -21,7 +21,7 @@ OUT_FILE = os.path.join(ROOT, "profiles", "pmc_handler.json")
 # the calibration engine of scripts/traffic_run.py calib: every launch moves
 # exactly CALIB_G * (CALIB_R * REPLICA_BYTES + GROUP_BYTES) bytes each way
 CALIB_G, CALIB_R = int(os.environ.get("TRAFFIC_GROUPS", "1000000")), 5
-REPLICA_BYTES, GROUP_BYTES = 4 * 13 + 8, 12
+REPLICA_BYTES, GROUP_BYTES = 64, 12          # abi.REPLICA_STATE_BYTES, GROUP_STATE_BYTES
 
 
 def kernels(d, counter=None):

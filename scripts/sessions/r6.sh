@@ -38,6 +38,13 @@ case $P in
       summ $OUT/s8_*.log $OUT/d20_*.log > $OUT/summary.txt
       TAG=r6_a step pmch 900 bash scripts/pmc_handler.sh
       ;;
+  b)  # the state quads (handler batches: 2-3 sectors per message, HBM tail cache): the GPU suite, the
+      # driver's command, the short shard's in-process A/B, the handler batches' calibrated traffic
+      step pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      step shard_ab 300 python -u scripts/shard_ab.py --groups 125000 --reps 15 --collective
+      TAG=r6_b step pmch 900 bash scripts/pmc_handler.sh
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0

@@ -18,7 +18,7 @@ import importlib  # noqa: E402
 abi = importlib.import_module("raft-kotlin_amd.abi")
 G = int(os.environ.get("TRAFFIC_GROUPS", "1000000"))
 R = 5
-REPLICA_BYTES = 4 * (abi.NUM_FIELDS + 3) + 8
+REPLICA_BYTES = abi.REPLICA_STATE_BYTES
 GROUP_BYTES = 12
 NCW = (abi.NUM_COUNTERS + 1) // 2
 

@@ -388,10 +388,13 @@ def test_traffic_probe_changes_nothing():
     co = o.step(40, nthreads=NTHREADS)[:, : abi.NUM_COUNTERS]
     assert np.array_equal(ce, co)
     d0, s0 = e.digest(), e.read_state()
-    state = kw["G"] * (5 * (4 * 13 + 8) + 12)
+    state = kw["G"] * (5 * abi.REPLICA_STATE_BYTES + abi.GROUP_STATE_BYTES)
     assert e.traffic_probe(0) == (state, state)
     phys = s0[:, [r * abi.NUM_FIELDS + abi.F_INDEX["phys"] for r in range(5)]]
     assert e.traffic_probe(1) == (4 * kw["G"] * 5, 8 * int(np.count_nonzero(phys < 96)))
+    # the handler batches' scattered-access probes: 2^21 sectors of 32 B, in engine scratch
+    assert e.traffic_probe(2) == (32 << 21, 0)
+    assert e.traffic_probe(3) == (0, 32 << 21)
     assert e.digest() == d0 and np.array_equal(e.read_state(), s0)
     ce = e.step(40)
     co = o.step(40, nthreads=NTHREADS)[:, : abi.NUM_COUNTERS]
