@@ -32,7 +32,7 @@ def main():
     st = e.read_state()
     max_term = int(st[:, [r * abi.NUM_FIELDS + abi.F_INDEX["term"] for r in range(R)]].max())
     rng = np.random.default_rng(12345)
-    group, dst, vote, app = bench.handler_requests(rng, N, G, R, max_term)
+    group, dst, vote, app = bench.legs().handler_requests(rng, N, G, R, max_term)
     dev = torch.device("cuda", 0)
     d_group, d_dst = torch.from_numpy(group).to(dev), torch.from_numpy(dst).to(dev)
     plan = []

@@ -126,7 +126,7 @@ def test_handler_requests_shapes_and_ranges():
     append [n, 8] as the structs' 32-bit words, half the appends at prev -1."""
     import numpy as np
     rng = np.random.default_rng(0)
-    g, d, v, a = bench.handler_requests(rng, 10_000, 50, 5, 7)
+    g, d, v, a = bench.legs().handler_requests(rng, 10_000, 50, 5, 7)
     assert g.shape == (10_000,) and d.dtype == np.int32 and v.shape == (10_000, 4) and a.shape == (10_000, 8)
     assert g.min() >= 0 and g.max() < 50 and d.min() >= 0 and d.max() < 5
     assert v.dtype == np.int32 and a.dtype == np.int32

@@ -54,6 +54,9 @@ def test_forced_collective_at_one_rank(backend, mode, monkeypatch):
         ar = out["timing"]["allreduce_ms"]
         assert ar is not None and 0 < ar < out["timing"]["wall_ms"], "the all-reduce runs inside the clock"
     assert out["valid"] and out["value"] > 0
+    # the kernel times come from an exact replay of the timed launches after the clock
+    assert out["timing"]["kernel_timing"] == "replay" and out["timing"]["replay_counters_equal"] is True
+    assert out["roofline"]["kernel_avg_ms"] > 0
     ca, cl = res["counters_all"], res["counters_local"]
     assert np.array_equal(ca, cl), "a one-rank all-reduce must return this rank's rows"
     kw = dict(abi.CONFIGS[3], G=G)
