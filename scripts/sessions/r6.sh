@@ -45,6 +45,19 @@ case $P in
       step shard_ab 300 python -u scripts/shard_ab.py --groups 125000 --reps 15 --collective
       TAG=r6_b step pmch 900 bash scripts/pmc_handler.sh
       ;;
+  c)  # the SALU / mask hand-off costs (ubench parts 5, 6); row 22's bound on the quad-layout kernel (every
+      # log store removed, results wrong, timing only) against production, interleaved; the driver's line
+      step ubench5 120 ./scripts/ubench/valu_rate5
+      step ubench6 120 ./scripts/ubench/valu_rate6
+      for i in 1 2; do
+        step prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_nostore.so step nostore_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        step prod_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_nostore.so step nostore_def_$i 200 python -u bench.py $Q
+      done
+      summ $OUT/prod_*.log $OUT/nostore_*.log > $OUT/summary.txt
+      step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
