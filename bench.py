@@ -329,6 +329,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target seconds of the SoA leg on every core")
     ap.add_argument("--cpu-seconds-1t", type=float, default=3.0, help="target seconds of each single-thread leg")
     ap.add_argument("--cpu-chunk", type=int, default=20)
+    ap.add_argument("--cpu-steady-at", type=int, default=9_600,
+                    help="the CPU baseline's steady-state window starts at this step (state from the GPU engine)")
+    ap.add_argument("--cpu-steady-steps", type=int, default=100, help="steps timed in that window (0 = skip)")
+    ap.add_argument("--cpu-steady-groups", type=int, default=50_000, help="groups of the steady-state sample")
     ap.add_argument("--plan-file", default="",
                     help="write the step-kernel launch sequence (leg, steps) and the workload key as JSON, for "
                          "attributing rocprofv3 dispatches (scripts/pmc_bench.sh)")
@@ -839,7 +843,7 @@ def main(argv=None, result=None):
                                                  log_cap, dev, G_local, R)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = legs().cpu_baseline(args, dict(kw, mode=mode, ae_max_entries=args.ae_max_entries), log_cap,
-                                           args.warmup + args.steps)
+                                                  args.warmup + args.steps, device=local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if result is not None:

@@ -243,6 +243,9 @@ def soa_lib():
             ("soa_read_state", C.c_int, [o, I64, I64, P(I32)]),
             ("soa_read_log", C.c_int, [o, I64, I64, P(I32), P(U32)]),
             ("soa_digest", C.c_uint64, [o]),
+            ("soa_write_state", C.c_int, [o, I64, I64, P(I32)]),
+            ("soa_write_log", C.c_int, [o, I64, I64, P(I32), P(U32)]),
+            ("soa_set_step_index", C.c_int, [o, I64]),
         ]:
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
@@ -293,3 +296,19 @@ class Soa:
 
     def digest(self) -> int:
         return int(soa_lib().soa_digest(self.h))
+
+    def write_state(self, state, g0=0):
+        a = np.ascontiguousarray(state, dtype=np.int32)
+        if soa_lib().soa_write_state(self.h, g0, a.shape[0], abi.ptr(a, C.c_int32)) != 0:
+            raise RuntimeError("soa_write_state")
+
+    def write_log(self, terms, cmds, g0=0):
+        t = np.ascontiguousarray(terms, dtype=np.int32)
+        c = np.ascontiguousarray(cmds, dtype=np.uint32)
+        if soa_lib().soa_write_log(self.h, g0, t.shape[0], abi.ptr(t, C.c_int32), abi.ptr(c, C.c_uint32)) != 0:
+            raise RuntimeError("soa_write_log")
+
+    def set_step_index(self, t):
+        """The index of the next step (its Philox counter c0), as the engine's."""
+        if soa_lib().soa_set_step_index(self.h, int(t)) != 0:
+            raise RuntimeError("soa_set_step_index")

@@ -485,6 +485,26 @@ void export_group(const soa* s, int64_t g, int32_t* w) {
     ex[1] = s->cmdc[g];
 }
 
+void import_group(soa* s, int64_t g, const int32_t* w) {
+    const int R = s->R;
+    for (int r = 0; r < R; ++r) {
+        const int64_t i = g * R + r;
+        const int32_t* f = w + r * RAFT_NUM_FIELDS;
+        s->term[i] = f[RAFT_F_TERM]; s->voted[i] = f[RAFT_F_VOTED]; s->role[i] = f[RAFT_F_ROLE];
+        s->commit[i] = f[RAFT_F_COMMIT]; s->last[i] = f[RAFT_F_LAST]; s->phys[i] = f[RAFT_F_PHYS];
+        s->elec[i] = f[RAFT_F_ELECTION_MS]; s->fl[i] = (uint32_t)f[RAFT_F_FLAGS];
+        s->phase[i] = f[RAFT_F_PHASE_MS]; s->retry[i] = f[RAFT_F_RETRY_MS];
+        for (int d = 0; d < R; ++d) {
+            s->nx[(size_t)i * R + d] = w[R * RAFT_NUM_FIELDS + r * R + d];
+            s->mc[(size_t)i * R + d] = w[R * RAFT_NUM_FIELDS + R * R + r * R + d];
+        }
+    }
+    const int32_t* ex = w + R * RAFT_NUM_FIELDS + 2 * R * R;
+    s->iso_rem[g] = ex[0] >> 8;
+    s->iso_rep[g] = ex[0] & 0xFF;
+    s->cmdc[g] = ex[1];
+}
+
 }  // namespace
 
 extern "C" {
@@ -575,6 +595,27 @@ int soa_read_log(const soa_t* s, int64_t g0, int64_t n, int32_t* terms, uint32_t
             cmds[i * row + j] = (int32_t)j < ph ? s->lc[src + j] : 0;
         }
     }
+    return RAFT_OK;
+}
+
+int soa_write_state(soa_t* s, int64_t g0, int64_t n, const int32_t* in) {
+    if (!s || g0 < 0 || n < 0 || g0 + n > s->G || !in) return RAFT_ERANGE;
+    const int32_t W = raft_group_words(s->R);
+    for (int64_t i = 0; i < n; ++i) import_group(s, g0 + i, in + (size_t)i * W);
+    return RAFT_OK;
+}
+
+int soa_write_log(soa_t* s, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds) {
+    if (!s || g0 < 0 || n < 0 || g0 + n > s->G || !terms || !cmds) return RAFT_ERANGE;
+    const size_t cells = (size_t)n * s->R * s->cap, at = (size_t)g0 * s->R * s->cap;
+    std::memcpy(s->lt.data() + at, terms, cells * sizeof(int32_t));
+    std::memcpy(s->lc.data() + at, cmds, cells * sizeof(uint32_t));
+    return RAFT_OK;
+}
+
+int soa_set_step_index(soa_t* s, int64_t t) {
+    if (!s || t < 0 || t > 0xFFFFFFFFll) return RAFT_EINVAL;
+    s->t = (uint32_t)t;
     return RAFT_OK;
 }
 

@@ -30,6 +30,13 @@ int  soa_step(soa_t* s, int32_t n_steps, int64_t* counters, int32_t nthreads);
 int  soa_read_state(const soa_t* s, int64_t g0, int64_t n, int32_t* out);
 int  soa_read_log(const soa_t* s, int64_t g0, int64_t n, int32_t* terms, uint32_t* cmds);
 uint64_t soa_digest(const soa_t* s);
+/* Restore a run exported at any step (the canonical [n][raft_group_words(R)]
+ * state, the [n][R][log_cap] logs, the next step's index): the steady-state
+ * CPU baseline resumes from the engine's state dump.  Every session row,
+ * primary or not, is held in full, so no primary owner is implied. */
+int  soa_write_state(soa_t* s, int64_t g0, int64_t n, const int32_t* in);
+int  soa_write_log(soa_t* s, int64_t g0, int64_t n, const int32_t* terms, const uint32_t* cmds);
+int  soa_set_step_index(soa_t* s, int64_t t);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,8 @@ import numpy as np
 import bench
 from bench import ROOT, HBM_PEAK_GBS, SCHEDULES, abi, available_cpus, cpu_model, grid_fill, shard, timed_leg
 
-def cpu_baseline(args, kw, log_cap, total_steps):
+
+def cpu_baseline(args, kw, log_cap, total_steps, device=0):
     """The CPU path on a bounded sample of the same workload, on this host's
     cores (rank 0, N=1 only): the SoA backend (oracle/raft_soa.cpp, the same
     step laid out as structure-of-arrays, std::thread over groups; `value`)
@@ -25,7 +26,14 @@ def cpu_baseline(args, kw, log_cap, total_steps):
     are bit-exact with each other and the engine.  A sample is a contiguous
     range of the same global groups, run for the same number of steps as the
     GPU (so logs grow exactly as they do there), sized by a short calibration
-    run to take about --cpu-seconds (--cpu-seconds-1t single-threaded)."""
+    run to take about --cpu-seconds (--cpu-seconds-1t single-threaded).
+
+    soa_steady / soa_steady_1t: the same SoA backend on the steady-state phase
+    mix (leader ticks dominate; the cold-start window above is the first
+    election storm): --cpu-steady-groups global groups are run on the GPU engine to
+    step --cpu-steady-at, their state and logs restored into the SoA backend,
+    and --cpu-steady-steps steps timed there; the engine runs the same steps
+    from the same state and the two digests must agree (matches_engine)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = args.cpu_threads or available_cpus()
@@ -56,10 +64,36 @@ def cpu_baseline(args, kw, log_cap, total_steps):
                 "sample": f"global groups 0..{G - 1}, the same {total_steps} steps as the GPU "
                           f"({args.warmup} untimed), {dt:.1f} s"}
 
+    def steady(nthreads):
+        eng_mod = importlib.import_module("raft-kotlin_amd.engine")
+        G, t0, n = args.cpu_steady_groups, args.cpu_steady_at, args.cpu_steady_steps
+        cap = int(64 + 0.3 * (t0 + n)) if kw["cmd_ppm"] < 1_000_000 else 64 + t0 + n
+        p = abi.make_params(log_cap=cap, **dict(kw, G=G))
+        e = eng_mod.RaftEngine(p, device=device)
+        e.step(t0, counters=False)                       # the GPU gets the sample to the window's start
+        o = O.Soa(abi.make_params(log_cap=cap, **dict(kw, G=G)))
+        o.write_state(e.read_state())
+        o.write_log(*e.read_log())
+        o.set_step_index(t0)
+        t = time.perf_counter()
+        o.step(n, nthreads=nthreads, counters=True)
+        dt = time.perf_counter() - t
+        e.step(n, counters=False)
+        same = e.digest() == o.digest()
+        e.close()
+        o.close()
+        return {"value": G * n / dt, "unit": "group-steps/s", "cores": nthreads, "matches_engine": same,
+                "window": [t0, t0 + n],
+                "sample": f"global groups 0..{G - 1}, steps {t0}..{t0 + n} (the steady state: state and logs at step "
+                          f"{t0} from the GPU engine), {dt:.2f} s"}
+
     legs = {}
     for name, cls in impls.items():
         legs[name] = timed(cls, threads, args.cpu_seconds if name == "soa" else args.cpu_seconds / 2)
         legs[name + "_1t"] = timed(cls, 1, args.cpu_seconds_1t)
+    if "soa" in impls and args.cpu_steady_steps > 0:
+        legs["soa_steady"] = steady(threads)
+        legs["soa_steady_1t"] = steady(1)
     best = legs["soa"] if "soa" in legs else legs["oracle"]
     return {"value": best["value"], "unit": "group-steps/s", "cores": threads, "kind": "port",
             "sample": ("oracle/raft_soa.cpp, the SoA CPU backend (bit-exact with the scalar restatement of "

@@ -49,6 +49,7 @@ case $P in
       # log store removed, results wrong, timing only) against production, interleaved; the driver's line
       step ubench5 120 ./scripts/ubench/valu_rate5
       step ubench6 120 ./scripts/ubench/valu_rate6
+      step pytest 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 240 --timeout-method thread -k "multi_chunk or non_direct or traffic_probe"
       for i in 1 2; do
         step prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
         RAFT_ENGINE_LIB=$PWD/raft-kotlin_amd/lib/libraft_engine_nostore.so step nostore_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q

@@ -862,6 +862,110 @@ def test_batch_status_between_batches(path):
     r.vote_batch(grp, dst, vq)                                          # inside the window: no status left over
 
 
+@pytest.mark.parametrize("path", ["bucketed", "sorted"])
+def test_ring_window_misses_in_a_multi_chunk_bucket(path):
+    """A bucket above the bucketed path's 512-message chunk, on a log_window
+    ring, whose every message reads below the window: 1,200 appends to the 8
+    replicas of one bucket (three chunks, runs of ~150 per replica), each
+    Log.get(prevLogIndex) a miss -- the batch reports exactly 1,200 (each chunk
+    adds its own to the count), and the vote batch after it reports nothing."""
+    pid = abi.BATCH_PATH_BUCKETED if path == "bucketed" else abi.BATCH_PATH_SORTED
+    R, G, W, cap2 = 5, 4, 16, 200
+    r = RaftEngine(abi.make_params(R=R, G=G, log_cap=cap2, log_window=W, seed=3))
+    r.set_batch_path(pid)
+    w2 = blank_groups(G, R)
+    for q in range(R):
+        set_fld(w2, R, q, "phys", np.full(G, 100))
+        set_fld(w2, R, q, "last", np.full(G, 100))
+        set_fld(w2, R, q, "term", np.full(G, 3))
+    r.write_state(w2)
+    r.write_log(np.full((G, R, cap2), 3, dtype=np.int32), np.zeros((G, R, cap2), dtype=np.uint32))
+    rng = np.random.default_rng(61)
+    n = 1200
+    key = rng.integers(0, 8, n)                                        # keys g * R + d in [0, 8): one bucket (S = 3)
+    grp, dst = (key // R).astype(np.int64), (key % R).astype(np.int32)
+    aq = np.zeros((n, 8), dtype=np.int64)
+    aq[:, 0], aq[:, 1], aq[:, 2], aq[:, 3] = 3, 1, 10, 3              # prevLogIndex 10 < physLen - W, no entry
+    with pytest.raises(RuntimeError, match=f"{n} log accesses below the retained log_window"):
+        r.append_batch(grp, dst, aq)
+    vq = np.zeros((n, 4), dtype=np.int32)
+    vq[:, 0], vq[:, 1], vq[:, 2], vq[:, 3] = 3, 1, 100, 3
+    r.vote_batch(grp, dst, vq)                                          # inside the window: no status left over
+
+
+def test_ring_multi_chunk_buckets_vs_oracle():
+    """Hot replicas on a wrapped 64-slot ring: 60 % of 8,000 messages go to 3
+    replicas of one bucket (a bucket of ~5,000 messages: ten 512-message
+    chunks applied in order by one workgroup), every access inside the window;
+    both batch paths against the oracle message by message."""
+    rng = np.random.default_rng(67)
+    R, G, cap, window, n = 5, 400, 160, 64, 8000
+    w, lt, lc = random_ring_states(rng, G, R, cap, window)
+    hot_g, hot_d = rng.integers(0, 3, n), rng.integers(0, 3, n)
+    grp, dst, vq, aq, cmd = handler_messages(rng, n, G, R, cap, w, window)
+    hot = rng.random(n) < 0.6
+    grp = np.where(hot, hot_g, grp)
+    dst = np.where(hot, hot_d, dst).astype(np.int32)
+    # every message's indices drawn against its own (final) target (handler_messages' rule)
+    last = np.array([fld(w[g], R, d, "last") for g, d in zip(grp, dst)])
+    phys = np.array([fld(w[g], R, d, "phys") for g, d in zip(grp, dst)])
+    vq[:, 2] = np.maximum(0, last - rng.integers(0, 4, n))
+    prev = last - 1 - rng.integers(0, window // 4, n)
+    prev = np.where(prev < phys - window + window // 4, np.maximum(last - 1, -1), prev)
+    aq[:, 2] = np.where((prev < 0) & (phys > window // 2), last - 1, np.maximum(prev, -1))
+    check_handler_batches(R, G, cap, window, abi.MODE_REFERENCE, w, lt, lc, grp, dst, vq, aq, cmd)
+
+
+def test_non_direct_gather_on_a_ring_vs_oracle_sample():
+    """The bucketed path's non-direct gather (more than 1,024 tiles: 4.2·10^6
+    messages) on a 64-slot log_window ring, the device entry points: the
+    responses of every message to 300 sampled groups, and those groups' final
+    state and logs, against the oracle's handlers applied in batch order."""
+    import torch
+    rng = np.random.default_rng(71)
+    R, G, cap, window, n = 5, 50_000, 160, 64, 4_200_000
+    w, lt, lc = random_ring_states(rng, G, R, cap, window)
+    e = RaftEngine(abi.make_params(R=R, G=G, log_cap=cap, log_window=window, seed=3))
+    e.write_state(w)
+    e.write_log(lt, lc)
+    grp = rng.integers(0, G, n)
+    dst = rng.integers(0, R, n).astype(np.int32)
+    NF = abi.NUM_FIELDS
+    last = w[grp, dst * NF + abi.F_INDEX["last"]]
+    phys = w[grp, dst * NF + abi.F_INDEX["phys"]]
+    prev = last - 1 - rng.integers(0, window // 4, n)
+    prev = np.where(prev < phys - window + window // 4, np.maximum(last - 1, -1), prev)
+    prev = np.where((prev < 0) & (phys > window // 2), last - 1, np.maximum(prev, -1))
+    aq = np.stack([rng.integers(0, 6, n), rng.integers(1, R + 1, n), prev, rng.integers(-1, 4, n),
+                   rng.integers(0, 2, n), rng.integers(0, 6, n), rng.integers(0, 1 << 32, n, dtype=np.uint64),
+                   rng.integers(0, 8, n)], axis=1).astype(np.int64).astype(np.uint32).view(np.int32)
+    dev = torch.device("cuda:0")
+    d_in = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (grp, dst, aq)]
+    d_resp = torch.zeros((n, 3), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    e.append_batch_dev(*(x.data_ptr() for x in d_in), d_resp.data_ptr(), n)
+    resp = d_resp.cpu().numpy()
+    # the oracle on 300 sampled groups: every message to them, in batch order
+    sample = np.sort(rng.choice(G, 300, replace=False))
+    local = {int(g): i for i, g in enumerate(sample)}
+    o = O.Oracle(abi.make_params(R=R, G=len(sample), log_cap=cap, log_window=window, seed=3))
+    o.write_state(w[sample])
+    o.write_log(lt[sample], lc[sample])
+    idx = np.flatnonzero(np.isin(grp, sample))
+    aqu = aq.view(np.uint32).astype(np.int64)
+    for m in idx:
+        q = aqu[m]
+        t_, s_, st_ = o.append(local[int(grp[m])], int(dst[m]), int(aq[m, 0]), int(aq[m, 1]), int(aq[m, 2]),
+                               int(aq[m, 3]), (int(aq[m, 5]), int(q[6])) if aq[m, 4] else None, int(aq[m, 7]))
+        assert tuple(int(x) for x in resp[m]) == (int(t_), int(s_), int(st_)), f"message {m}"
+    se = np.concatenate([e.read_state(int(g), 1) for g in sample])
+    assert_same_state(se, o.read_state(), R, "sampled groups after the 4.2e6-message batch")
+    t_e = np.concatenate([e.read_log(int(g), 1)[0] for g in sample])
+    c_e = np.concatenate([e.read_log(int(g), 1)[1] for g in sample])
+    assert_same_logs(se, (t_e, c_e), o.read_log(), R, "sampled groups' logs")
+    assert len(idx) > 20_000                                            # ~84 messages per sampled group
+
+
 def test_batch_paths_agree_at_scale():
     """4.2·10^6 votes over 10^6 groups of 5 (the bucketed path's bucket-count
     cap applies: S is raised until at most 16384 buckets remain), then 10^6

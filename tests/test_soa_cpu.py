@@ -37,3 +37,21 @@ def test_soa_refuses_what_it_does_not_model():
         O.Soa(abi.make_params(R=3, G=4, mode=abi.MODE_TEXTBOOK))
     with pytest.raises(ValueError):
         O.Soa(abi.make_params(R=3, G=4, log_cap=64, log_window=16))
+
+
+def test_soa_restore_resumes_bit_exact():
+    """soa_write_state / soa_write_log / soa_set_step_index (the steady-state
+    CPU baseline's restore, bench_legs.cpu_baseline): a run exported at step
+    t and restored into a fresh backend continues exactly as the original."""
+    kw = dict(abi.CONFIGS[3], G=300)
+    a = O.Soa(abi.make_params(log_cap=200, **kw))
+    a.step(300, nthreads=4)
+    b = O.Soa(abi.make_params(log_cap=200, **kw))
+    b.write_state(a.read_state())
+    b.write_log(*a.read_log())
+    b.set_step_index(300)
+    assert b.digest() == a.digest()
+    assert np.array_equal(a.step(50, nthreads=4), b.step(50, nthreads=2))
+    assert a.digest() == b.digest()
+    a.close()
+    b.close()
