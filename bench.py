@@ -331,7 +331,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-chunk", type=int, default=20)
     ap.add_argument("--cpu-steady-at", type=int, default=9_600,
                     help="the CPU baseline's steady-state window starts at this step (state from the GPU engine)")
-    ap.add_argument("--cpu-steady-steps", type=int, default=100, help="steps timed in that window (0 = skip)")
+    ap.add_argument("--cpu-steady-steps", type=int, default=400, help="steps timed in that window (0 = skip)")
     ap.add_argument("--cpu-steady-groups", type=int, default=50_000, help="groups of the steady-state sample")
     ap.add_argument("--plan-file", default="",
                     help="write the step-kernel launch sequence (leg, steps) and the workload key as JSON, for "

@@ -59,6 +59,23 @@ case $P in
       summ $OUT/prod_*.log $OUT/nostore_*.log > $OUT/summary.txt
       step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       ;;
+  d)  # the VOP3 select rewrite (scripts/variants/cndmask_e64.py): the GPU suite on the rewritten build,
+      # then production / the identity-rewrite control / the rewrite, interleaved, on the driver's command
+      # and the default
+      L=$PWD/raft-kotlin_amd/lib
+      RAFT_ENGINE_LIB=$L/libraft_engine_e64.so step pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      for i in 1 2 3; do
+        step prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_asmid.so step asmid_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_e64.so step e64_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+      done
+      for i in 1 2; do
+        step prod_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_asmid.so step asmid_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_e64.so step e64_def_$i 200 python -u bench.py $Q
+      done
+      summ $OUT/prod_*.log $OUT/asmid_*.log $OUT/e64_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0

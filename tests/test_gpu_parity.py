@@ -919,7 +919,7 @@ def test_ring_multi_chunk_buckets_vs_oracle():
 def test_non_direct_gather_on_a_ring_vs_oracle_sample():
     """The bucketed path's non-direct gather (more than 1,024 tiles: 4.2·10^6
     messages) on a 64-slot log_window ring, the device entry points: the
-    responses of every message to 300 sampled groups, and those groups' final
+    responses of every message to 300 consecutive groups, and those groups' final
     state and logs, against the oracle's handlers applied in batch order."""
     import torch
     rng = np.random.default_rng(71)
@@ -945,10 +945,12 @@ def test_non_direct_gather_on_a_ring_vs_oracle_sample():
     torch.cuda.synchronize(dev)
     e.append_batch_dev(*(x.data_ptr() for x in d_in), d_resp.data_ptr(), n)
     resp = d_resp.cpu().numpy()
-    # the oracle on 300 sampled groups: every message to them, in batch order
-    sample = np.sort(rng.choice(G, 300, replace=False))
+    # the oracle on 300 consecutive groups (their global ids key the timer
+    # draws): every message to them, in batch order
+    s0 = int(rng.integers(0, G - 300))
+    sample = np.arange(s0, s0 + 300)
     local = {int(g): i for i, g in enumerate(sample)}
-    o = O.Oracle(abi.make_params(R=R, G=len(sample), log_cap=cap, log_window=window, seed=3))
+    o = O.Oracle(abi.make_params(R=R, G=len(sample), g0=s0, log_cap=cap, log_window=window, seed=3))
     o.write_state(w[sample])
     o.write_log(lt[sample], lc[sample])
     idx = np.flatnonzero(np.isin(grp, sample))
