@@ -399,9 +399,10 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     # ---- timed region ----
     # The launches' own start / stop timestamps (hipExtLaunchKernelGGL events)
     # cost ~10 us of host time at the first launch (profiles/r6_b shard_ab):
-    # by default (--kernel-timing replay) the timed region carries none, and
-    # the kernel times come from an exact replay of the same launches after
-    # the clock (below); --kernel-timing region times the region's own.
+    # by default (--kernel-timing replay) the timed region carries no event at
+    # all, and the kernel and all-reduce times come from an exact replay of
+    # the same launches after the clock (below); --kernel-timing region times
+    # the region's own.
     # RAFT_BENCH_NO_KERNEL_EVENTS=1: no kernel times at all (A/B runs).
     no_ev = os.environ.get("RAFT_BENCH_NO_KERNEL_EVENTS") == "1"
     timing = args.kernel_timing == "region" and not no_ev
@@ -443,20 +444,29 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
                 dist.all_reduce(gcounters[done:done + k])
             if done + k < args.steps:
                 eng.wait_stream(comm_stream.cuda_stream)
+    # the clock's own instrumentation: none with --kernel-timing replay (the
+    # all-reduce's events too are recorded around its replay, below)
+    instr = timing or no_ev
+
+    def allreduce_end(src, dst, events):
+        if events:
+            ar0.record(stream)
+        if comm is not None:
+            eng.allreduce_counters(comm, src.data_ptr(), dst.data_ptr(), args.steps)
+        else:
+            with torch.cuda.stream(stream):
+                dst.copy_(src)
+                dist.all_reduce(dst)
+        if events:
+            ar1.record(stream)
     if mode == "end":
         # the default: every timed row all-reduced once, in series on the
         # engine stream after the last launch's counter reduction (nothing
         # runs beside the RCCL kernel), before the closing sync.  The copy
         # keeps this rank's own rows for its roofline.
-        ar0.record(stream)
-        if comm is not None:
-            eng.allreduce_counters(comm, rows[0], gcounters.data_ptr(), args.steps)
-        else:
-            with torch.cuda.stream(stream):
-                gcounters.copy_(counters)
-                dist.all_reduce(gcounters)
-        ar1.record(stream)
-    ev1.record(stream)
+        allreduce_end(counters, gcounters, instr)
+    if instr or args.sync == "spin":
+        ev1.record(stream)
     if args.sync == "spin":
         # the host polls the region's last event before the closing device
         # sync: a blocking wait sleeps on an interrupt once the runtime's short
@@ -476,7 +486,7 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
             torch.cuda.synchronize(dev)
             after_ms = (time.perf_counter() - t_ar) * 1e3
     ev_ms = eng.timed_span(ev1.cuda_event) if timing else None
-    allreduce_ms = ar0.elapsed_time(ar1) if mode == "end" else (after_ms if mode == "after" else None)
+    allreduce_ms = ar0.elapsed_time(ar1) if mode == "end" and instr else (after_ms if mode == "after" else None)
     kern_ms, launches = eng.kernel_time()
     eng.set_kernel_timing(False)
     replay_equal = None
@@ -493,8 +503,12 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
         eng.set_kernel_timing(True)
         for done, k in plan:
             eng.step_async(k, rcount[done].data_ptr())
+        if mode == "end":                         # the all-reduce's time, from its replay
+            allreduce_end(rcount, torch.zeros_like(gcounters), True)
         kern_ms, launches = eng.kernel_time()
         eng.set_kernel_timing(False)
+        if mode == "end":
+            allreduce_ms = ar0.elapsed_time(ar1)
         replay_equal = bool(torch.equal(rcount, counters))
 
     elapsed = max(wall, ev_ms / 1e3) if ev_ms is not None else wall

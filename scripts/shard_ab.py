@@ -4,9 +4,11 @@ driver's 20-step command): ONE engine, the bench's own timed region
 all-reduce inside the clock, the closing sync) repeated --reps times per
 variant, the variants interleaved and each repetition from step 0
 (raft_engine_reset), so box-to-box and run-to-run drift cancel.  Variants:
-the launches' own timestamps on / off (RAFT_BENCH_NO_KERNEL_EVENTS) x the
-closing wait (--sync block / spin).  With --collective the one-rank RCCL
-all-reduce runs inside the clock (the bench's RAFT_BENCH_FORCE_COLLECTIVE).
+where the timestamps are (--kernel-timing region: on the timed launches and
+around the all-reduce, inside the clock; replay: none inside the clock, the
+times from a replay after it) x the closing wait (--sync block / spin).
+With --collective the one-rank RCCL all-reduce runs inside the clock (the
+bench's RAFT_BENCH_FORCE_COLLECTIVE).
 Prints one JSON line: the median wall / stream-event / kernel times per variant.
 
     python scripts/shard_ab.py --groups 125000 --reps 15 --collective
@@ -32,7 +34,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--collective", action="store_true")
-    ap.add_argument("--variants", default="ev1_block,ev1_spin,ev0_block,ev0_spin")
+    ap.add_argument("--variants", default="region_block,replay_block,replay_spin")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -50,14 +52,17 @@ def main():
     out = {v: [] for v in a.variants.split(",")}
     for rep in range(a.reps):
         for v in out:
-            ev, sync = v.split("_")
-            os.environ["RAFT_BENCH_NO_KERNEL_EVENTS"] = "1" if ev == "ev0" else "0"
-            args = bench.parse_args(["--steps", str(a.steps), "--warmup", str(a.warmup), "--sync", sync])
+            kt, sync = v.split("_")
+            args = bench.parse_args(["--steps", str(a.steps), "--warmup", str(a.warmup), "--sync", sync,
+                                     "--kernel-timing", kt])
             eng.reset()
             leg = bench.timed_leg(eng, args, L, a.collective, dev, 1, comm)
             out[v].append({"wall_ms": leg["wall"] * 1e3, "ev_ms": leg["ev_ms"], "kern_ms": leg["kern_avg_ms"],
                            "allreduce_ms": leg["allreduce_ms"]})
-    res = {v: {k: statistics.median(x[k] for x in rows) for k in ("wall_ms", "ev_ms", "kern_ms")} |
+    def med(rows, k):
+        xs = [x[k] for x in rows if x[k] is not None]
+        return statistics.median(xs) if xs else None
+    res = {v: {k: med(rows, k) for k in ("wall_ms", "ev_ms", "kern_ms", "allreduce_ms")} |
            {"wall_ms_all": [round(x["wall_ms"], 4) for x in rows]} for v, rows in out.items()}
     print(json.dumps({"groups": a.groups, "steps": a.steps, "reps": a.reps, "collective": a.collective,
                       "variants": res}))
