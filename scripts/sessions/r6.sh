@@ -76,6 +76,18 @@ case $P in
       done
       summ $OUT/prod_*.log $OUT/asmid_*.log $OUT/e64_*.log > $OUT/summary.txt
       ;;
+  e)  # the short shard with no event inside the clock (replay timing) against the round-5 region timing,
+      # in process; its timeline under the runtime trace; the driver's command
+      step shard_ab 400 python -u scripts/shard_ab.py --groups 125000 --reps 15 --collective
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step trace_s8 300 rocprofv3 --kernel-trace --hip-runtime-trace -d $OUT/trace_s8 -o run --output-format csv -- python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      TIMELINE_STEP=-3 python scripts/trace_timeline.py $OUT/trace_s8 > $OUT/timeline_s8.json 2> $OUT/timeline_s8.err || true
+      rm -rf $OUT/trace_s8
+      for i in 1 2; do
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        step d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+      done
+      summ $OUT/s8_*.log $OUT/d20_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0

@@ -9,6 +9,7 @@ to the end of the synchronisation that follows it, on the same clock.
 """
 import csv
 import glob
+import os
 import json
 import sys
 
@@ -26,7 +27,9 @@ def main(d):
     steps = [i for i, r in enumerate(rows) if "step_kernel" in r[2]]
     if not steps:
         raise SystemExit("no step_kernel dispatch")
-    i0 = steps[-1]
+    # TIMELINE_STEP: which step_kernel dispatch (bench.py --kernel-timing
+    # replay runs the timed launch again after the clock: -3 is the timed one)
+    i0 = steps[int(os.environ.get("TIMELINE_STEP", "-1"))]
     t0 = rows[i0][0]
     gpu = [{"kernel": k, "start_us": (a - t0) / 1e3, "end_us": (b - t0) / 1e3, "dur_us": (b - a) / 1e3}
            for a, b, k in rows[i0:i0 + 8]]
