@@ -88,6 +88,20 @@ case $P in
       done
       summ $OUT/s8_*.log $OUT/d20_*.log > $OUT/summary.txt
       ;;
+  f)  # the handler batches with their requests staged by the tile kernel (gathered into LDS with the keys;
+      # an append's log[prev] read with the state): the batch tests, then the bench's handler leg against
+      # the previous batch design (prevh), interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      step pytest 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "handler or batch or ring_window or non_direct or wire or service"
+      for i in 1 2 3; do
+        step new_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_prevh.so step prevh_$i 200 python -u bench.py $H
+      done
+      for f in $OUT/new_*.log $OUT/prevh_*.log; do
+        python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
+      done > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
