@@ -132,47 +132,35 @@ __global__ __launch_bounds__(BLOCK) void batch_keys_kernel(const int64_t* __rest
 }
 
 // One replica's run of messages, in batch order: load the replica (idx =
-// g * R + r), apply the messages at sorted positions m = m0, m0 + 1, ... while
-// more(m) -- request reqat(m), response index rix(m) -- and store it back.
-// Shared by both batch paths (batch_kernel: the requests from the caller's
-// array; bucket_batch_kernel: from the workgroup's LDS).
+// g * R + r), apply message ord(m) for m = m0, m0 + 1, ... while more(m), store
+// it back.  Shared by both batch paths (batch_kernel, bucket_batch_kernel).
 // flags[1]: accesses below the retained log window (RAFT_EWINDOW)
-template <int kind>
-using ReqOf = std::conditional_t<kind == BATCH_VOTE, raft_vote_req,
-                                 std::conditional_t<kind == BATCH_APPEND, raft_append_req, uint32_t>>;
-template <bool TB, int kind, class More, class ReqAt, class Rix>
-__device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_t idx, int m0, More more, ReqAt reqat,
-                                          Rix rix, void* resp, unsigned int* flags, unsigned int* hmiss = nullptr) {
-    using Req = ReqOf<kind>;
+template <bool TB, int kind, class More, class Ord>
+__device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_t idx, int m0, More more, Ord ord,
+                                          const void* req, void* resp, unsigned int* flags,
+                                          unsigned int* hmiss = nullptr) {
+    using Req = std::conditional_t<kind == BATCH_VOTE, raft_vote_req,
+                                   std::conditional_t<kind == BATCH_APPEND, raft_append_req, uint32_t>>;
     const int R = p.R;
     const int64_t i = idx / R;
     const int r = (int)(idx - i * R);
     const uint32_t gid = (uint32_t)(p.g0 + i);
     constexpr bool VO = kind == BATCH_VOTE;
-    // the run's first request is fetched with the replica's quads (one round
+    // the run's first request is fetched with the replica's fields (one round
     // trip for both); each later one while the previous message is applied
-    Req q = reqat(m0);
-    uint32_t om = rix(m0);
+    uint32_t om = ord(m0);
+    Req q = ((const Req*)req)[om];
     RepState x;
     RepQuads o;
     load_rep<VO>(x, o, p, idx);
     const LogView lv = log_of(p, idx);
-    // append: the first message's log[prevLogIndex], read with the quads
-    // (speculatively: used only if 0 <= prev < lastIndex and the tail cache
-    // does not hold it); a later message of the run reads its own after the
-    // earlier ones' log writes
-    int32_t pre = 0;
-    if constexpr (kind == BATCH_APPEND) {
-        const int32_t pv = q.prev_log_index;
-        if (pv >= 0 && (lv.W != FLAT_W || pv < lv.cap)) pre = (int32_t)lv.at(pv)->x;
-    }
     BatchCounters cnt;
     for (int m = m0;;) {
         const Req qm = q;
         const uint32_t oc = om;
         if (more(m + 1)) {
-            q = reqat(m + 1);
-            om = rix(m + 1);
+            om = ord(m + 1);
+            q = ((const Req*)req)[om];
         }
         if constexpr (kind == BATCH_VOTE) {
             int32_t rt;
@@ -188,7 +176,7 @@ __device__ __forceinline__ void apply_run(const DevParams& p, uint32_t t, int64_
             // log[prev] (and TB: log[prev + 1]) from the tail cache when it
             // holds them, else from the log
             const int32_t dprev = pv == x.last - 1 ? x.t1 : pv == x.last - 2 ? x.t2
-                                  : (pv >= 0 && pv < x.last) ? (m == m0 ? pre : (int32_t)lv.at(pv)->x) : 0;
+                                  : (pv >= 0 && pv < x.last) ? (int32_t)lv.at(pv)->x : 0;
             const int32_t dnext = !TB ? 0 : pv + 1 == x.last - 1 ? x.t1 : pv + 1 == x.last - 2 ? x.t2
                                   : (pv + 1 >= 0 && pv + 1 < x.last) ? (int32_t)lv.at(pv + 1)->x : 0;
             const uint64_t thrown = append_handler<TB, true>(x.ref(), __ballot(1), r + 1, lv, qm.term, qm.leader_id,
@@ -223,10 +211,8 @@ __global__ __launch_bounds__(BLOCK) void batch_kernel(DevParams p, uint32_t t, i
     if (m0 >= n || *(volatile unsigned int*)&flags[0]) return;
     const Key key = keys[m0];
     if (m0 > 0 && keys[m0 - 1] == key) return;                          // not the first of its run
-    using Req = ReqOf<kind>;
     apply_run<TB, kind>(p, t, (int64_t)key, m0, [&](int m) { return m < n && keys[m] == key; },
-                        [&](int m) { return ((const Req*)req)[order[m]]; }, [&](int m) { return order[m]; }, resp,
-                        flags);
+                        [&](int m) { return order[m]; }, req, resp, flags);
 }
 
 // ---- the bucketed path (uint32 keys): a stable partition of each tile instead
@@ -270,17 +256,9 @@ constexpr int GATHER_TILES = 2 * BUCKET_THREADS;                        // bucke
 // match by ballots over the bucket bits), plus the wave's earlier rounds (the
 // wave's LDS count, read by every lane of the match and then advanced by its
 // lowest lane), plus the earlier waves (their counts, summed after the tile).
-// QW: 32-bit words of a request (vote 4, append 8, command 1): each
-// message's request is moved to its partitioned place too (treq, [tile
-// messages][QW]), so that bucket_batch_kernel gathers it with the message's
-// key -- in the same round trip -- instead of fetching it by message index
-// from the caller's array when it applies it.
-template <int QW>
 __global__ __launch_bounds__(TILE_THREADS) void bucket_tile_kernel(const int64_t* __restrict__ group,
-                                                            const int32_t* __restrict__ dst,
-                                                            const uint32_t* __restrict__ req, int req_a16, int n,
-                                                            int64_t G, int R, int S, int NB, int bbits,
-                                                            uint2* __restrict__ tiles, uint32_t* __restrict__ treq,
+                                                            const int32_t* __restrict__ dst, int n, int64_t G, int R,
+                                                            int S, int NB, int bbits, uint2* __restrict__ tiles,
                                                             uint2* __restrict__ seg, unsigned int* dflags,
                                                             unsigned int* hflags) {
     // LDS: the tile's output staged (written out coalesced: one 8-B store per
@@ -302,22 +280,11 @@ __global__ __launch_bounds__(TILE_THREADS) void bucket_tile_kernel(const int64_t
     uint32_t key[TILE_IPT], rk[TILE_IPT];
     int64_t gg[TILE_IPT];
     int32_t dd[TILE_IPT];
-    uint32_t rq[TILE_IPT][QW];
 #pragma unroll
     for (int j = 0; j < TILE_IPT; ++j) {
         const int m = min(base + j * 64, n - 1);
         gg[j] = group[m];
         dd[j] = dst[m];
-        if (QW % 4 == 0 && req_a16) {                                  // (a caller's array may be 4-B aligned only)
-#pragma unroll
-            for (int w = 0; w < QW; w += 4) {
-                const uint4 v = *(const uint4*)&req[(int64_t)m * QW + w];
-                rq[j][w] = v.x; rq[j][w + 1] = v.y; rq[j][w + 2] = v.z; rq[j][w + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int w = 0; w < QW; ++w) rq[j][w] = req[(int64_t)m * QW + w];
-        }
     }
     bool bad = false;
 #pragma unroll
@@ -378,17 +345,7 @@ __global__ __launch_bounds__(TILE_THREADS) void bucket_tile_kernel(const int64_t
         const int m = base + j * 64;
         if (m < n) {
             const uint32_t b = key[j] >> S;
-            const uint32_t at = off[b] + cw[b] + rk[j];
-            stage[at] = make_uint2(key[j], (uint32_t)m);                 // (key, message index)
-            uint32_t* const d = treq + ((int64_t)t0 + at) * QW;          // its request, at the same place
-            if constexpr (QW % 4 == 0) {
-#pragma unroll
-                for (int w = 0; w < QW; w += 4)
-                    *(uint4*)&d[w] = make_uint4(rq[j][w], rq[j][w + 1], rq[j][w + 2], rq[j][w + 3]);
-            } else {
-#pragma unroll
-                for (int w = 0; w < QW; ++w) d[w] = rq[j][w];
-            }
+            stage[off[b] + cw[b] + rk[j]] = make_uint2(key[j], (uint32_t)m);   // (key, message index)
         }
     }
     __syncthreads();
@@ -399,17 +356,12 @@ __global__ __launch_bounds__(TILE_THREADS) void bucket_tile_kernel(const int64_t
     }
 }
 
-template <int kind>
-constexpr int req_words() { return (int)(sizeof(ReqOf<kind>) / 4); }
 template <bool TB, int kind, int NT>
 __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t t, int n, int S, int NB, int ntile,
                                                           const uint2* __restrict__ tiles,
-                                                          const uint32_t* __restrict__ treq,
-                                                          const uint2* __restrict__ seg, void* resp,
-                                                          unsigned int* dflags, unsigned int* hflags) {
+                                                          const uint2* __restrict__ seg, const void* req,
+                                                          void* resp, unsigned int* dflags, unsigned int* hflags) {
     static_assert(2 * NT >= GATHER_TILES, "the direct gather holds at most two tiles per thread");
-    constexpr int QW = req_words<kind>();
-    using Req = ReqOf<kind>;
     using Sort = rocprim::block_radix_sort<uint32_t, NT, 1, uint32_t>;
     using Scan = rocprim::block_scan<uint32_t, NT>;
     __shared__ union {
@@ -418,19 +370,6 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
     } sm;
     __shared__ uint2 buf[NT];
     __shared__ uint32_t lk[NT], lo[NT];
-    // the chunk's messages before the sort, by chunk position: message index
-    // and request (the sort permutes positions; a run reads its requests here)
-    __shared__ uint32_t lmsg[NT];
-    __shared__ __attribute__((aligned(16))) uint32_t lreq[NT * QW];
-    auto copy_req = [&](int to, int64_t from) {                      // treq[from] -> lreq[to]
-        if constexpr (QW % 4 == 0) {
-#pragma unroll
-            for (int w = 0; w < QW; w += 4) *(uint4*)&lreq[to * QW + w] = *(const uint4*)&treq[from * QW + w];
-        } else {
-#pragma unroll
-            for (int w = 0; w < QW; ++w) lreq[to * QW + w] = treq[from * QW + w];
-        }
-    };
     __shared__ uint32_t spos[GATHER_TILES], soff[GATHER_TILES];
     // a message outside the engine (bucket_tile_kernel): nothing is applied
     const bool bad = *(volatile unsigned int*)&dflags[0] != 0u;         // the same for the whole grid
@@ -467,11 +406,7 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
             for (int q = tt0; q < tt1 && at < c0 + len; ++q) {
                 const uint2 sg = seg[(int64_t)q * NB + bk];
                 const uint32_t lo_i = max(at, c0), hi_i = min(at + sg.y, c0 + (uint32_t)len);
-                for (uint32_t i = lo_i; i < hi_i; ++i) {
-                    const int64_t P = (int64_t)q * TILE + sg.x + (i - at);
-                    buf[i - c0] = tiles[P];
-                    copy_req((int)(i - c0), P);
-                }
+                for (uint32_t i = lo_i; i < hi_i; ++i) buf[i - c0] = tiles[(int64_t)q * TILE + sg.x + (i - at)];
                 at += sg.y;
             }
         }
@@ -487,15 +422,12 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
                     const int mid = (lo_t + hi_t) >> 1;
                     if (spos[mid] <= i) lo_t = mid; else hi_t = mid;
                 }
-                const int64_t P = (int64_t)lo_t * TILE + soff[lo_t] + (i - spos[lo_t]);
-                x = tiles[P];
-                copy_req(q, P);
+                x = tiles[(int64_t)lo_t * TILE + soff[lo_t] + (i - spos[lo_t])];
             } else {
                 x = buf[q];
             }
-            lmsg[q] = x.y;
         }
-        uint32_t k[1] = {x.x - kb}, v[1] = {(uint32_t)q};                 // sorted: the chunk positions
+        uint32_t k[1] = {x.x - kb}, v[1] = {x.y};
         Sort().sort(k, v, sm.sort, 0, S + 1);
         lk[q] = k[0];
         lo[q] = v[0];
@@ -503,8 +435,7 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
         if (q < len && (q == 0 || lk[q - 1] != lk[q])) {
             const uint32_t key = lk[q];
             apply_run<TB, kind>(p, t, (int64_t)(kb + key), q, [&](int m) { return m < len && lk[m] == key; },
-                                [&](int m) { return *(const Req*)&lreq[lo[m] * QW]; },
-                                [&](int m) { return lmsg[lo[m]]; }, resp, dflags + 1,    // misses -> dflags[2]
+                                [&](int m) { return lo[m]; }, req, resp, dflags + 1,    // misses -> dflags[2]
                                 hflags + 1);
         }
         // another chunk of this bucket: the barrier (a workgroup-scope fence:
@@ -559,15 +490,8 @@ static int run_batch_keys(raft_engine* e, int kind, const int64_t* group, const 
     return RAFT_OK;
 }
 
-using BK = void (*)(DevParams, uint32_t, int, int, int, int, const uint2*, const uint32_t*, const uint2*, void*,
+using BK = void (*)(DevParams, uint32_t, int, int, int, int, const uint2*, const uint2*, const void*, void*,
                     unsigned int*, unsigned int*);
-using TK = void (*)(const int64_t*, const int32_t*, const uint32_t*, int, int, int64_t, int, int, int, int, uint2*,
-                    uint32_t*, uint2*, unsigned int*, unsigned int*);
-static TK tile_kernel_of(int kind) {
-    return kind == BATCH_VOTE ? bucket_tile_kernel<req_words<BATCH_VOTE>()>
-           : kind == BATCH_APPEND ? bucket_tile_kernel<req_words<BATCH_APPEND>()>
-                                  : bucket_tile_kernel<req_words<BATCH_COMMAND>()>;
-}
 static BK bucket_kernel_of(int kind, bool tb) {
     constexpr int NT = BUCKET_THREADS;
     return kind == BATCH_VOTE     ? (tb ? bucket_batch_kernel<true, BATCH_VOTE, NT> : bucket_batch_kernel<false, BATCH_VOTE, NT>)
@@ -591,16 +515,12 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
     int bbits = 1;
     while ((uint64_t)(NB - 1) >> bbits) ++bbits;
     const int ntile = (int)ntile64;
-    const int qw = kind == BATCH_VOTE ? req_words<BATCH_VOTE>() : kind == BATCH_APPEND ? req_words<BATCH_APPEND>()
-                                                                                      : req_words<BATCH_COMMAND>();
     const size_t b_t = al256((size_t)ntile * TILE * 8), b_s = al256((size_t)NB * ntile * 8);
-    const size_t b_q = al256((size_t)ntile * TILE * 4 * qw);
     const size_t sz0 = e->bst_bytes;                                    // grow_dev reallocates only to grow
-    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, BST_HEAD + b_t + b_s + b_q)) return rc;
+    if (int rc = grow_dev(e, &e->bst, &e->bst_bytes, BST_HEAD + b_t + b_s)) return rc;
     char* b = e->bst + BST_HEAD;
     uint2* tiles = (uint2*)b; b += b_t;
     uint2* seg = (uint2*)b; b += b_s;
-    uint32_t* treq = (uint32_t*)b; b += b_q;
     // status words: dflags (device: [0] a message outside the engine, [2]
     // the window misses), zero between batches; hflags = the engine's
     // page-locked words [0], [1] (RAFT_ERANGE; "some miss was counted"),
@@ -618,16 +538,14 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
     // (more than 64 KB of dynamic LDS: allowed once per device)
     static std::atomic<bool> lds_set[64];
     if (e->device < 0 || e->device >= 64 || !lds_set[e->device].load(std::memory_order_acquire)) {
-        for (int k = BATCH_VOTE; k <= BATCH_COMMAND; ++k)
-            HIP_TRY(hipFuncSetAttribute((const void*)tile_kernel_of(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)((size_t)TILE * 8 + (size_t)(TILE_WAVES + 1) * BUCKETS_MAX * 2)));
+        HIP_TRY(hipFuncSetAttribute((const void*)bucket_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)((size_t)TILE * 8 + (size_t)(TILE_WAVES + 1) * BUCKETS_MAX * 2)));
         if (e->device >= 0 && e->device < 64) lds_set[e->device].store(true, std::memory_order_release);
     }
-    tile_kernel_of(kind)<<<ntile, TILE_THREADS, tile_lds, e->stream>>>(
-        group, dst, (const uint32_t*)req, ((uintptr_t)req & 15) == 0 ? 1 : 0, n, e->p.G, e->p.R, S, NB, bbits, tiles,
-        treq, seg, dflags, hflags);
+    bucket_tile_kernel<<<ntile, TILE_THREADS, tile_lds, e->stream>>>(
+        group, dst, n, e->p.G, e->p.R, S, NB, bbits, tiles, seg, dflags, hflags);
     const BK kern = bucket_kernel_of(kind, e->p.mode == RAFT_MODE_TEXTBOOK);
-    kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, treq, seg, resp, dflags,
+    kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, dflags,
                                                hflags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(e->stream));
