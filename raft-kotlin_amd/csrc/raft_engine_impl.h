@@ -66,9 +66,11 @@ struct raft_engine {
     int schedule, sched_wg;
     bool part_only;             // the workload's kernel is partitions-only (auto_subranges)
     raft_kernel_info last;      // the last step launch (raft_engine_kernel_info)
-    const void* occ_kern;       // workgroups per CU of occ_kern at occ_lds bytes of LDS (cached)
-    size_t occ_lds;
-    int occ_wg;
+    static constexpr int OCC_SLOTS = 4;
+    const void* occ_kern[OCC_SLOTS];   // workgroups per CU of occ_kern at occ_lds bytes of LDS (cached)
+    size_t occ_lds[OCC_SLOTS];
+    int occ_wg[OCC_SLOTS];
+    uint32_t occ_next;
     uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials (buffer 0)
     uint32_t* partials2;        // buffer 1: launches alternate between the two when nsub > 1
     // launch sub-ranges (raft_engine_step_async): the step workgroups split

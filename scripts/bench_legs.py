@@ -13,7 +13,41 @@ import time
 import numpy as np
 
 import bench
-from bench import ROOT, HBM_PEAK_GBS, SCHEDULES, abi, available_cpus, cpu_model, grid_fill, shard, timed_leg
+from bench import (ROOT, HBM_PEAK_GBS, SCHEDULES, abi, algorithmic_bytes, available_cpus, cpu_model, grid_fill,
+                   load_pmc, shard, state_crossing_bytes, timed_leg)
+
+
+def streaming_leg(eng, args, dev, G, R, pmc_key):
+    """One step per launch (--stream-steps launches, one sub-range): every
+    launch streams the whole group state HBM -> VGPRs -> HBM, the HBM-bound
+    formulation SURVEY.md §8(d) prices.  Returns (its roofline object, the
+    overflow / window-miss count of its steps)."""
+    import torch
+    eng.set_steps_per_launch(1)
+    eng.set_subranges(1)                      # one full-grid launch per step
+    sc = torch.zeros((args.stream_steps, abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
+    eng.set_kernel_timing(True)
+    eng.step_async(args.stream_steps, sc.data_ptr())
+    eng.sync()
+    s_ms, s_n = eng.kernel_time()
+    eng.set_kernel_timing(False)
+    cs = sc.cpu().numpy()[:, : abi.NUM_COUNTERS]
+    s_avg = s_ms / max(1, s_n)
+    s_bytes = algorithmic_bytes(cs, G, R) / max(1, s_n)
+    s_state = state_crossing_bytes(cs, G, R, s_n) / max(1, s_n)
+    s_ach = s_bytes / (s_avg / 1e3) / 1e9
+    s_pmc = load_pmc(dict(pmc_key, launch_steps=1, leg="streaming", stream_steps=args.stream_steps))
+    bad = int(cs[:, abi.C_INDEX["log_overflow"]].sum() + cs[:, abi.C_INDEX["log_window_miss"]].sum())
+    out = {"steps_per_launch": 1, "steps": args.stream_steps, "kernel_avg_ms": s_avg,
+           "alg_bytes_per_launch": s_bytes, "achieved": s_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": s_ach / HBM_PEAK_GBS,
+           "traffic": s_pmc["hbm_bytes_per_launch"] if s_pmc else None,
+           "traffic_frac": (s_pmc["hbm_bytes_per_launch"] / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS if s_pmc else None),
+           "state_bytes_per_launch": s_state,
+           "achieved_state_crossing": s_state / (s_avg / 1e3) / 1e9,
+           "frac_state_crossing": s_state / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS,
+           "kernel_group_steps_per_s": G / (s_avg / 1e3)}
+    return out, bad
 
 
 def cpu_baseline(args, kw, log_cap, total_steps, device=0):

@@ -102,6 +102,19 @@ case $P in
         python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
       done > $OUT/summary.txt
       ;;
+  g)  # the untimed rehearsal and the occupancy cache: the GPU suite, standalone short-shard runs (the
+      # driver's kind: one timed region per process) and the driver's command
+      step pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      for i in 1 2 3; do
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8norh_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 --no-rehearse $Q
+      done
+      for i in 1 2; do
+        step d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+      done
+      summ $OUT/s8_*.log $OUT/s8norh_*.log $OUT/d20_*.log > $OUT/summary.txt
+      step bench_driver 400 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
