@@ -314,6 +314,7 @@ def parse_args(argv=None):
                          "own launches (region: the timestamps are then inside the clock)")
     ap.add_argument("--no-rehearse", dest="rehearse", action="store_false",
                     help="skip the untimed rehearsal of the timed launches (then raft_engine_reset) before the warmup")
+    ap.add_argument("--rehearse-ms", type=float, default=50.0, help="minimum wall time of the rehearsal's repeats")
     ap.add_argument("--sync", choices=["spin", "block"], default="block",
                     help="how the host waits for the timed region's last work before the closing device sync: "
                          "poll its event (spin) or the runtime's blocking wait alone (block)")
@@ -371,6 +372,7 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     wcount = torch.zeros((max(1, args.warmup), abi.COUNTER_STRIDE), dtype=torch.int64, device=dev)
     mode = args.allreduce if coll else None
     plan = [(q, min(chunk, args.steps - q)) for q in range(0, args.steps, chunk)]
+    rehearsals = 0
 
     # ---- rehearsal (untimed, before the warmup): the timed region's launches
     # and its all-reduce once, on scratch rows, then raft_engine_reset back to
@@ -380,14 +382,22 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     # 1/8 shard (profiles/r6_e shard_ab).  The warmup and the timed region
     # then run exactly as without it, from the same state.
     if args.rehearse and args.steps:
-        scratch = torch.zeros_like(counters)
-        for done, k in plan:
-            eng.step_async(k, scratch[done].data_ptr())
-        if mode == "end" and comm is not None:
-            eng.allreduce_counters(comm, scratch.data_ptr(), torch.zeros_like(scratch).data_ptr(), args.steps)
-        eng.sync()
-        eng.reset()
-        del scratch
+        # repeated for at least --rehearse-ms of wall time, so the GPU's clocks
+        # are out of their idle state (a short first region ran its kernel
+        # ~4 % slower than later ones in the same process, profiles/r6_g)
+        scratch, sglob = torch.zeros_like(counters), torch.zeros_like(counters)
+        t_r = time.perf_counter()
+        while True:
+            rehearsals += 1
+            for done, k in plan:
+                eng.step_async(k, scratch[done].data_ptr())
+            if mode == "end" and comm is not None:
+                eng.allreduce_counters(comm, scratch.data_ptr(), sglob.data_ptr(), args.steps)
+            eng.sync()
+            eng.reset()
+            if (time.perf_counter() - t_r) * 1e3 >= args.rehearse_ms:
+                break
+        del scratch, sglob
 
     # ---- warmup (untimed) ----
     comm_stream = torch.cuda.Stream(device=dev)
@@ -544,7 +554,8 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
         kern_avg_per_rank = [kern_avg_ms]
     return {"wall": wall, "ev_ms": ev_ms, "kern_ms": kern_ms, "launches": launches, "elapsed": elapsed,
             "kern_avg_ms": kern_avg_ms, "kern_avg_per_rank": kern_avg_per_rank, "allreduce_ms": allreduce_ms,
-            "counters": counters, "gcounters": gcounters, "wcount": wcount, "replay_counters_equal": replay_equal}
+            "counters": counters, "gcounters": gcounters, "wcount": wcount, "replay_counters_equal": replay_equal,
+            "rehearsals": rehearsals}
 
 
 def main(argv=None, result=None):
@@ -712,11 +723,20 @@ def main(argv=None, result=None):
                 probes.append([kind, *eng.traffic_probe(kind)])
     if args.plan_file and rank == 0:
         # [leg, steps, dispatches]: a launch of the warmup / timed legs is one
-        # step-kernel dispatch per sub-range; the streaming leg runs one range
-        seq = [["warmup", x, nsub] for x in launch_plan(args.warmup, L)] + [["timed", x, nsub] for x in timed_plan]
-        if general is not None:                   # the general kernel replays the warmup and timed launches
-            seq += [["general_warmup", x, nsub] for x in launch_plan(args.warmup, L)]
-            seq += [["general", x, nsub] for x in timed_plan]
+        # step-kernel dispatch per sub-range; the streaming leg runs one range.
+        # Each timed_leg: the rehearsal (the timed launches), the warmup, the
+        # timed launches, then the replay of warmup + timed (kernel timing)
+        def leg_seq(name, reps):
+            w = [[f"{name}warmup", x, nsub] for x in launch_plan(args.warmup, L)]
+            t = [[f"{name}timed" if name else "timed", x, nsub] for x in timed_plan]
+            r = [[f"{name}rehearsal", x, nsub] for x in timed_plan] * reps
+            rp = ([[f"{name}replay_warmup", x, nsub] for x in launch_plan(args.warmup, L)]
+                  + [[f"{name}replay", x, nsub] for x in timed_plan]) if args.kernel_timing == "replay" else []
+            return r + w + t + rp
+        seq = leg_seq("", leg["rehearsals"])
+        if general is not None:                   # the general kernel runs the same leg from step 0
+            seq += [["general" if x[0] == "general_timed" else x[0], *x[1:]]
+                    for x in leg_seq("general_", general["rehearsals"])]
         seq += [["streaming", 1, 1]] * args.stream_steps
         ix = abi.C_INDEX
         stores = float(c_loc[:, ix["entry_writes"]].sum() + c_loc[:, ix["commands"]].sum()) / max(1, launches)
@@ -820,6 +840,11 @@ def main(argv=None, result=None):
                     "binding roofline. roofline_streaming is the same step at one step per launch",
         },
         "roofline_valu": roofline_valu,
+        # what binds the fused launch (roofline is §8(d)'s algorithmic-bytes
+        # figure, not an HBM measurement): instruction issue, DESIGN.md §4.6
+        "bound_by": {"resource": "SIMD instruction issue (VALU + SALU, ~2.6 + ~2.0 SIMD-cycles each)",
+                     "valu_frac_of_nominal": roofline_valu["frac"] if roofline_valu else None,
+                     "hbm_traffic_frac": (traffic / (kern_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None)},
         "general_kernel": general,
         "roofline_streaming": streaming,
         "timing": {"wall_ms": wall * 1e3, "stream_event_ms": ev_ms, "step_kernel_ms_total": kern_ms,

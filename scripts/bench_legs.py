@@ -381,7 +381,7 @@ def general_kernel_leg(eng, args, chunk, dev, main_rows, main_kern_avg_ms):
     return {"value": eng.G * args.steps / leg["elapsed"], "unit": "group-steps/s",
             "kernel_net": info["net"], "kernel_avg_ms": leg["kern_avg_ms"],
             "kernel_time_vs_specialised": leg["kern_avg_ms"] / main_kern_avg_ms if main_kern_avg_ms else None,
-            "counters_equal_main_leg": bool(np.array_equal(rows, main_rows)),
+            "counters_equal_main_leg": bool(np.array_equal(rows, main_rows)), "rehearsals": leg["rehearsals"],
             "note": "the same warmup, steps and launches on the same engine (reset to step 0) with the general "
                     "step kernel (NET_ALL: drops, partitions and isolation churn decided at run time, the command "
                     "harness read from the parameters); the main leg's kernel is built for the workload "

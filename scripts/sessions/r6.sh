@@ -115,6 +115,28 @@ case $P in
       summ $OUT/s8_*.log $OUT/s8norh_*.log $OUT/d20_*.log > $OUT/summary.txt
       step bench_driver 400 python -u bench.py --gpus 1 --steps 20 --warmup 5
       ;;
+  h)  # the rehearsal's duration (GPU clocks out of idle before a short timed region), standalone runs as
+      # the driver makes them; the tile kernel at 2,048 messages per tile (handler batches)
+      L=$PWD/raft-kotlin_amd/lib
+      for i in 1 2 3; do
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_r50_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_r0_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 --rehearse-ms 0 $Q
+      done
+      for i in 1 2; do
+        step d20_r50_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        step d20_r0_$i 200 python -u bench.py --steps 20 --warmup 5 --rehearse-ms 0 $Q
+      done
+      summ $OUT/s8_*.log $OUT/d20_*.log > $OUT/summary.txt
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      for i in 1 2; do
+        step prod_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_t512x4.so step t512x4_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_t256x8.so step t256x8_$i 200 python -u bench.py $H
+      done
+      for f in $OUT/prod_*.log $OUT/t512x4_*.log $OUT/t256x8_*.log; do
+        python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
+      done > $OUT/handler_summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
