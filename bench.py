@@ -6,7 +6,13 @@ seeded 5% message drop, leader-isolation churn (1e-3 per group-step, 15
 steps), one client command per group-step with probability 1/4.  A "step" is
 one lockstep heartbeat period of every group: timers, the
 RequestVote phase, the AppendEntries/commit phase and client commands, with
-all state resident in HBM before the timed region starts.
+all state resident in HBM before the timed region starts.  Before the W
+warmup steps, an untimed rehearsal runs the timed launches on scratch counter
+rows and resets the engine to step 0, repeated for >= --rehearse-ms (50 ms),
+so a short timed region does not run on the GPU's idle clocks; the warmup and
+the timed K steps then run from the same state as without it.  Nothing inside
+the clock is instrumented: kernel and all-reduce times come from a replay of
+the same launches after it (--kernel-timing replay).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -694,13 +700,10 @@ def main(argv=None, result=None):
             "effective_clock_ghz": clk,
             "cycle_split": cycle_split(pmc),
             "source": pmc["source"],
-            "note": "SQ_INSTS_VALU of this exact launch and kernel build (rocprofv3 --pmc, same workload, launch "
-                    "length and kernel sources) / the live average launch time; peak = 1024 SIMDs x 2.4 GHz / 2 "
-                    "cycles per wave64 VALU instruction (MI355X_MICROARCH.md), the rate of the cheapest (VOP2) "
-                    "instructions; this kernel's mix is mostly VOP3 compares, lane-mask selects and 64-bit "
-                    "multiplies at 4.1-4.7 cycles each (profiles/r1_v7/ubench). cycle_split is the measured, "
-                    "disjoint split of the waves' cycles (SQ_ACTIVE_INST_ANY issuing, SQ_WAIT_ANY parked on "
-                    "s_waitcnt/barrier, SQ_WAIT_INST_ANY ready but not issued; MI355X_MICROARCH.md SQ block)",
+            "note": "SQ_INSTS_VALU of this exact launch and kernel build (rocprofv3 --pmc) / the live launch time; "
+                    "peak = 1024 SIMDs x 2.4 GHz / 2 cycles (the cheapest VALU); this mix averages ~2.6 cycles per "
+                    "VALU plus ~2 per SALU (DESIGN.md §4.6); cycle_split: SQ_ACTIVE_INST_ANY / SQ_WAIT_ANY / "
+                    "SQ_WAIT_INST_ANY over SQ_WAVE_CYCLES",
         }
 
     # ---- the general kernel (untimed for `value`): the warmup and timed legs
@@ -832,12 +835,10 @@ def main(argv=None, result=None):
             "state_bytes_per_launch": bytes_state / max(1, launches),
             "achieved_state_crossing": achieved_state,
             "frac_state_crossing": achieved_state / HBM_PEAK_GBS,
-            "note": "alg_equiv: achieved = SURVEY.md §8(d) algorithmic bytes per group-step (event counts from "
-                    "this rank's own kernel counters) x the group-steps of one launch / the launch's live average "
-                    "duration. A fused launch keeps every replica in VGPRs for its steps, so the HBM bytes it "
-                    "really moves (traffic, PMC of this exact launch, null if none was recorded) are far below "
-                    "the algorithmic bytes: traffic_frac is the measured HBM fraction, and roofline_valu is the "
-                    "binding roofline. roofline_streaming is the same step at one step per launch",
+            "note": "alg_equiv: SURVEY.md §8(d) algorithmic bytes per group-step (this rank's own kernel counters) "
+                    "x the group-steps of one launch / the launch's average duration; the fused launch keeps the "
+                    "replicas in VGPRs, so its real HBM bytes (traffic, PMC) are far below: traffic_frac is the "
+                    "measured HBM fraction, bound_by / roofline_valu the binding resource",
         },
         "roofline_valu": roofline_valu,
         # what binds the fused launch (roofline is §8(d)'s algorithmic-bytes
@@ -850,20 +851,13 @@ def main(argv=None, result=None):
         "timing": {"wall_ms": wall * 1e3, "stream_event_ms": ev_ms, "step_kernel_ms_total": kern_ms,
                    "allreduce_ms": leg["allreduce_ms"], "kernel_timing": args.kernel_timing,
                    "replay_counters_equal": leg["replay_counters_equal"],
-                   "note": "the timed region: each rank's wall clock from after the opening barrier + device "
-                           "sync to after its closing device sync (the closing barrier follows the clock; the job's "
-                           "time is the MAX over ranks); the launches inside it carry no timestamps (kernel_timing "
-                           "replay): step_kernel_ms_total (the time during which a step kernel ran, the union of the "
-                           "sub-range launches) comes from the same launches replayed from step 0 after the clock, "
-                           "each with its own start / stop timestamps on the engine stream, whose counter rows equal "
-                           "the region's (replay_counters_equal). With kernel_timing region the region's own launches "
-                           "carry them, and ms_per_step uses the larger of wall and stream_event_ms (the first "
-                           "launch's start timestamp to an event after the last work). The rest of the wall is launch "
-                           "latency, the counter reductions, the counter all-reduce and the final sync. allreduce_ms: "
-                           "the all-reduce of the timed counter rows (with its row copy), stream events around it on "
-                           "the engine stream; inside the clock unless counter_allreduce_every says after_timed_"
-                           "region_diagnostic (then host time after the clock stopped); null at one rank without a "
-                           "collective"},
+                   "rehearsals": leg["rehearsals"], "rehearse_ms": args.rehearse_ms,
+                   "note": "each rank's wall clock from after the opening barrier + device sync to after its closing "
+                           "device sync (the job's time is the MAX over ranks); nothing inside it is instrumented "
+                           "(kernel_timing replay): the kernel and all-reduce times come from the same launches "
+                           "replayed from step 0 after the clock, whose counter rows equal the region's; before the "
+                           "warmup an untimed rehearsal of the timed launches (then a reset) runs for >= "
+                           "--rehearse-ms, so the GPU leaves its idle clocks (DESIGN.md §5)"},
         "valid": overflow == 0 and wmiss == 0 and bad_untimed == 0,
         "safety": safety,
         "counters_last_step": {n: int(v) for n, v in zip(abi.COUNTER_NAMES, c_all[-1])},
