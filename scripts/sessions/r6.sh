@@ -137,6 +137,23 @@ case $P in
         python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
       done > $OUT/handler_summary.txt
       ;;
+  i)  # the rehearsal's length on the driver's command and the 1/8 shard; the N = 2 rehearsal (gloo ranks on
+      # one GPU) through the rehearsal / replay path; the other workloads for the results table
+      for i in 1 2; do
+        for r in 0 50 200 1000; do
+          step d20_r${r}_$i 200 python -u bench.py --steps 20 --warmup 5 --rehearse-ms $r $Q
+        done
+        for r in 50 200; do
+          RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_r${r}_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 --rehearse-ms $r $Q
+        done
+      done
+      summ $OUT/d20_*.log $OUT/s8_*.log > $OUT/summary.txt
+      TAG=r6_i/dist STEPS=512 step dist 900 bash scripts/dist_rehearsal.sh
+      step cfg5 300 python -u bench.py --config 5 --groups 100000 --no-cpu-baseline --handler-batch 0
+      step cfg2 300 python -u bench.py --config 2 --groups 10000 --no-cpu-baseline --handler-batch 0
+      step textbook 300 python -u bench.py --mode textbook --no-cpu-baseline --handler-batch 0
+      summ $OUT/cfg5.log $OUT/cfg2.log $OUT/textbook.log > $OUT/summary_other.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
