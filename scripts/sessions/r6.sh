@@ -154,6 +154,24 @@ case $P in
       step textbook 300 python -u bench.py --mode textbook --no-cpu-baseline --handler-batch 0
       summ $OUT/cfg5.log $OUT/cfg2.log $OUT/textbook.log > $OUT/summary_other.txt
       ;;
+  j)  # the scalar-compare fold (scripts/variants/scc_fold.py: an s_cmp of a mask the logic op before it
+      # just computed, dropped, its branch inverted): the GPU suite on the rewritten build, then
+      # production / the identity-rewrite control / the fold, interleaved, on the driver's command and
+      # the default
+      L=$PWD/raft-kotlin_amd/lib
+      RAFT_ENGINE_LIB=$L/libraft_engine_scc.so step pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      for i in 1 2 3; do
+        step prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_asmid.so step asmid_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_scc.so step scc_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+      done
+      for i in 1 2; do
+        step prod_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_asmid.so step asmid_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_scc.so step scc_def_$i 200 python -u bench.py $Q
+      done
+      summ $OUT/prod_*.log $OUT/asmid_*.log $OUT/scc_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
