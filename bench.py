@@ -41,6 +41,7 @@ from __future__ import annotations
 import argparse
 import importlib
 import json
+import math
 import os
 import socket
 import subprocess
@@ -381,28 +382,37 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     rehearsals = 0
 
     # ---- rehearsal (untimed, before the warmup): the timed region's launches
-    # and its all-reduce once, on scratch rows, then raft_engine_reset back to
-    # step 0.  The first use of each launch shape and of the collective's path
-    # (host-side setup) happens here instead of inside the clock: the first
-    # timed region of a process measured ~8 us above the later ones at the
-    # 1/8 shard (profiles/r6_e shard_ab).  The warmup and the timed region
-    # then run exactly as without it, from the same state.
+    # and its all-reduce on scratch rows, then raft_engine_reset to step 0, so
+    # the launch shapes' and the collective's first use (~8 us at the 1/8
+    # shard, profiles/r6_e) and the GPU's idle clocks (a short first region's
+    # kernel ran ~4 % slow, r6_g) stay off the clock.  Repeated for at least
+    # --rehearse-ms; a repeat may hold the RCCL all-reduce, so every rank runs
+    # the same count: from the second repeat's time (the first pays the first
+    # use), MAX over the ranks.
     if args.rehearse and args.steps:
-        # repeated for at least --rehearse-ms of wall time, so the GPU's clocks
-        # are out of their idle state (a short first region ran its kernel
-        # ~4 % slower than later ones in the same process, profiles/r6_g)
         scratch, sglob = torch.zeros_like(counters), torch.zeros_like(counters)
-        t_r = time.perf_counter()
-        while True:
-            rehearsals += 1
+
+        def rehearse_once():
             for done, k in plan:
                 eng.step_async(k, scratch[done].data_ptr())
             if mode == "end" and comm is not None:
                 eng.allreduce_counters(comm, scratch.data_ptr(), sglob.data_ptr(), args.steps)
             eng.sync()
             eng.reset()
-            if (time.perf_counter() - t_r) * 1e3 >= args.rehearse_ms:
-                break
+        t_r = time.perf_counter()
+        rehearse_once()
+        t_2 = time.perf_counter()
+        rehearse_once()
+        t_e = time.perf_counter()
+        left_ms = args.rehearse_ms - (t_e - t_r) * 1e3
+        more = max(0, math.ceil(left_ms / max(1e-3, (t_e - t_2) * 1e3))) if left_ms > 0 else 0
+        if coll:
+            mt = torch.tensor([more], dtype=torch.int64, device=dev)
+            dist.all_reduce(mt, op=dist.ReduceOp.MAX)
+            more = int(mt.item())
+        for _ in range(more):
+            rehearse_once()
+        rehearsals = 2 + more
         del scratch, sglob
 
     # ---- warmup (untimed) ----
