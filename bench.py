@@ -65,6 +65,9 @@ VALU_PEAK_GIPS = SIMDS * CLOCK_HZ / VALU_CYCLES / 1e9
 # primary-session column (nextIndex, matchIndex) in 4 int32 quads; per group: 3 harness words
 REPLICA_BYTES, GROUP_BYTES = abi.REPLICA_STATE_BYTES, abi.GROUP_STATE_BYTES
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_rows.json")
+# group-steps/s the rehearsal count assumes (above every measured rate: its
+# repeats last at least --rehearse-ms)
+REHEARSE_RATE = 3.0e10
 SCHEDULES = {"auto": abi.SCHED_AUTO, "one": abi.SCHED_ONE_PER_WAVE, "balanced": abi.SCHED_BALANCED}
 
 
@@ -321,7 +324,8 @@ def parse_args(argv=None):
                          "own launches (region: the timestamps are then inside the clock)")
     ap.add_argument("--no-rehearse", dest="rehearse", action="store_false",
                     help="skip the untimed rehearsal of the timed launches (then raft_engine_reset) before the warmup")
-    ap.add_argument("--rehearse-ms", type=float, default=50.0, help="minimum wall time of the rehearsal's repeats")
+    ap.add_argument("--rehearse-ms", type=float, default=50.0,
+                    help="the rehearsal's length: repeats of REHEARSE_RATE-priced work lasting at least this")
     ap.add_argument("--sync", choices=["spin", "block"], default="block",
                     help="how the host waits for the timed region's last work before the closing device sync: "
                          "poll its event (spin) or the runtime's blocking wait alone (block)")
@@ -385,34 +389,26 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     # and its all-reduce on scratch rows, then raft_engine_reset to step 0, so
     # the launch shapes' and the collective's first use (~8 us at the 1/8
     # shard, profiles/r6_e) and the GPU's idle clocks (a short first region's
-    # kernel ran ~4 % slow, r6_g) stay off the clock.  Repeated for at least
-    # --rehearse-ms; a repeat may hold the RCCL all-reduce, so every rank runs
-    # the same count: from the second repeat's time (the first pays the first
-    # use), MAX over the ranks.
+    # kernel ran ~4 % slow, r6_g) stay off the clock.  Repeated for about
+    # --rehearse-ms: the count is fixed by the planned work (group-steps at
+    # REHEARSE_RATE, faster than any measured rate, so the repeats last at
+    # least that long), the same in every run of one command (rocprofv3's
+    # passes) and, as MAX over the ranks, on every rank (a repeat may hold
+    # the RCCL all-reduce)
     if args.rehearse and args.steps:
         scratch, sglob = torch.zeros_like(counters), torch.zeros_like(counters)
-
-        def rehearse_once():
+        rehearsals = max(1, math.ceil(args.rehearse_ms / 1e3 * REHEARSE_RATE / (eng.G * args.steps)))
+        if coll:
+            mt = torch.tensor([rehearsals], dtype=torch.int64, device=dev)
+            dist.all_reduce(mt, op=dist.ReduceOp.MAX)
+            rehearsals = int(mt.item())
+        for _ in range(rehearsals):
             for done, k in plan:
                 eng.step_async(k, scratch[done].data_ptr())
             if mode == "end" and comm is not None:
                 eng.allreduce_counters(comm, scratch.data_ptr(), sglob.data_ptr(), args.steps)
             eng.sync()
             eng.reset()
-        t_r = time.perf_counter()
-        rehearse_once()
-        t_2 = time.perf_counter()
-        rehearse_once()
-        t_e = time.perf_counter()
-        left_ms = args.rehearse_ms - (t_e - t_r) * 1e3
-        more = max(0, math.ceil(left_ms / max(1e-3, (t_e - t_2) * 1e3))) if left_ms > 0 else 0
-        if coll:
-            mt = torch.tensor([more], dtype=torch.int64, device=dev)
-            dist.all_reduce(mt, op=dist.ReduceOp.MAX)
-            more = int(mt.item())
-        for _ in range(more):
-            rehearse_once()
-        rehearsals = 2 + more
         del scratch, sglob
 
     # ---- warmup (untimed) ----
