@@ -172,6 +172,21 @@ case $P in
       done
       summ $OUT/prod_*.log $OUT/asmid_*.log $OUT/scc_*.log > $OUT/summary.txt
       ;;
+  k)  # handler batches: runs found without the LDS sort in buckets of <= 2^11 replicas (the chunk kept in
+      # batch order, a run led by its first position): the batch tests, then the handler leg against the
+      # previous revision's library (hprev), interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+          -k "handler or batch or bucket or ring or gather"
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      for i in 1 2 3; do
+        step prod_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_hprev.so step hprev_$i 200 python -u bench.py $H
+      done
+      for f in $OUT/prod_*.log $OUT/hprev_*.log; do
+        python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
+      done > $OUT/handler_summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
