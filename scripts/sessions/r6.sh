@@ -187,6 +187,20 @@ case $P in
         python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
       done > $OUT/handler_summary.txt
       ;;
+  l)  # the tile kernel at 1,024 threads x 4 messages (16 waves, 4 per SIMD; same 4,096-message tile)
+      # against production, interleaved, on the bench's handler leg
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      RAFT_ENGINE_LIB=$L/libraft_engine_t1024x4.so step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu \
+          -x -v --timeout 300 --timeout-method thread -k "handler or batch or bucket or ring or gather"
+      for i in 1 2 3; do
+        step prod_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_t1024x4.so step t1024x4_$i 200 python -u bench.py $H
+      done
+      for f in $OUT/prod_*.log $OUT/t1024x4_*.log; do
+        python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
+      done > $OUT/handler_summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
