@@ -970,7 +970,7 @@ def test_non_direct_gather_on_a_ring_vs_oracle_sample():
 
 def test_batch_paths_agree_at_scale():
     """4.2·10^6 votes over 10^6 groups of 5 (the bucketed path's bucket-count
-    cap applies: S is raised until at most 16384 buckets remain), then 10^6
+    cap applies: S is raised until at most 3,072 buckets remain), then 10^6
     appends: the bucketed and the sorted path leave the same responses, state
     and logs."""
     import torch
