@@ -362,6 +362,20 @@ def parse_args(argv=None):
     return args
 
 
+def rehearsal_count(rehearse_ms, groups, steps, coll=False, dev="cpu"):
+    """The rehearsal's repeats: this rank's group-steps priced at REHEARSE_RATE
+    fill rehearse_ms; with `coll` the MAX over the ranks, so every rank runs
+    the same number of the repeats' collectives (tests/test_dist_cpu.py)."""
+    n = max(1, math.ceil(rehearse_ms / 1e3 * REHEARSE_RATE / max(1, groups * steps)))
+    if coll:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n = int(t.item())
+    return n
+
+
 def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     """Warmup (untimed), then the timed region of `args.steps` lockstep steps on
     `eng`: enqueued in chunks of `chunk` steps, bracketed by a barrier and a
@@ -389,19 +403,11 @@ def timed_leg(eng, args, chunk, coll, dev, world, comm=None):
     # and its all-reduce on scratch rows, then raft_engine_reset to step 0, so
     # the launch shapes' and the collective's first use (~8 us at the 1/8
     # shard, profiles/r6_e) and the GPU's idle clocks (a short first region's
-    # kernel ran ~4 % slow, r6_g) stay off the clock.  Repeated for about
-    # --rehearse-ms: the count is fixed by the planned work (group-steps at
-    # REHEARSE_RATE, faster than any measured rate, so the repeats last at
-    # least that long), the same in every run of one command (rocprofv3's
-    # passes) and, as MAX over the ranks, on every rank (a repeat may hold
-    # the RCCL all-reduce)
+    # kernel ran ~4 % slow, r6_g) stay off the clock; repeated for at least
+    # --rehearse-ms, the count fixed by the planned work (rehearsal_count)
     if args.rehearse and args.steps:
         scratch, sglob = torch.zeros_like(counters), torch.zeros_like(counters)
-        rehearsals = max(1, math.ceil(args.rehearse_ms / 1e3 * REHEARSE_RATE / (eng.G * args.steps)))
-        if coll:
-            mt = torch.tensor([rehearsals], dtype=torch.int64, device=dev)
-            dist.all_reduce(mt, op=dist.ReduceOp.MAX)
-            rehearsals = int(mt.item())
+        rehearsals = rehearsal_count(args.rehearse_ms, eng.G, args.steps, coll, dev)
         for _ in range(rehearsals):
             for done, k in plan:
                 eng.step_async(k, scratch[done].data_ptr())

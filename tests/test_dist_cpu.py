@@ -56,3 +56,31 @@ def test_two_rank_sharding_equals_single():
     cf = full.step(STEPS)[:, : abi.NUM_COUNTERS]
     np.testing.assert_array_equal(counters, cf)
     assert digest % (1 << 64) == full.digest()
+
+
+def rehearsal_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    # uneven shards whose own counts differ (600 vs 601 repeats of 20 steps)
+    own = bench.rehearsal_count(50.0, 125_001 - 2 * rank, 20)
+    q.put((rank, own, bench.rehearsal_count(50.0, 125_001 - 2 * rank, 20, coll=True)))
+    dist.destroy_process_group()
+
+
+def test_rehearsal_count_agreed_over_ranks():
+    """bench.py's rehearsal repeats a launch sequence that holds the RCCL
+    counter all-reduce, so every rank must run the same number of repeats:
+    ranks whose own counts differ agree on the MAX."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=rehearsal_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][1] != got[1][1]                       # the ranks' own counts differ
+    assert got[0][2] == got[1][2] == max(got[0][1], got[1][1])
