@@ -201,6 +201,20 @@ case $P in
         python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
       done > $OUT/handler_summary.txt
       ;;
+  m)  # the handler batch kernel's bucket size: ~640 messages per bucket (2^12 replicas, 1,221 buckets:
+      # 1.2 rounds of the resident workgroups, two chunks each) and ~160 (2^10, 4,883 buckets) against
+      # production's ~410 (2^11, 2,442 buckets: 2.4 rounds), interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      for i in 1 2 3; do
+        step prod_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_bm640.so step bm640_$i 200 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_bm160.so step bm160_$i 200 python -u bench.py $H
+      done
+      for f in $OUT/prod_*.log $OUT/bm640_*.log $OUT/bm160_*.log; do
+        python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
+      done > $OUT/handler_summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
