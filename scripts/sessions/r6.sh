@@ -215,6 +215,18 @@ case $P in
         python -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1])['handler_batch']; print('$(basename $f)', *('%s %.4e %.4f bad=%d' % (k, d[k]['messages_per_s_device'], d[k]['ms_per_batch_device'], d[k]['parity_mismatches']) for k in ('vote', 'append')))"
       done > $OUT/handler_summary.txt
       ;;
+  n)  # launch sub-ranges on the balanced schedule at the default (10^4 steps, 400-step launches): the
+      # grid split over 2 or 3 streams whose launches overlap at the launch boundaries, against one
+      for i in 1 2; do
+        for sr in 1 2 3; do
+          step def_sr${sr}_$i 200 python -u bench.py --subranges $sr $Q
+        done
+      done
+      for sr in 2 3; do
+        step d20_sr${sr} 200 python -u bench.py --steps 20 --warmup 5 --subranges $sr $Q
+      done
+      summ $OUT/def_*.log $OUT/d20_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
