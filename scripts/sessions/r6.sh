@@ -227,6 +227,27 @@ case $P in
       done
       summ $OUT/def_*.log $OUT/d20_*.log > $OUT/summary.txt
       ;;
+  o)  # launch length at the default (10^4 steps): 50 / 100 / 200 / 400 steps per launch, twice each,
+      # interleaved -- how much of a launch's time is its boundary (tail, state in / out)
+      for i in 1 2; do
+        for k in 50 100 200 400; do
+          step def_k${k}_$i 200 python -u bench.py --steps-per-launch $k $Q
+        done
+      done
+      summ $OUT/def_*.log > $OUT/summary.txt
+      ;;
+  p)  # long launches, timing only (scripts/variants/long_launch_timing.patch: the counter rows wrap every
+      # 400 steps in LDS, so a launch may run 2,000 steps; its counters are wrong): the default at 400 /
+      # 1,000 / 2,000 steps per launch against production's 400
+      L=$PWD/raft-kotlin_amd/lib
+      for i in 1 2; do
+        step prod_k400_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_ll.so step ll_k400_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_ll.so step ll_k1000_$i 200 python -u bench.py --steps-per-launch 1000 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_ll.so step ll_k2000_$i 200 python -u bench.py --steps-per-launch 2000 $Q
+      done
+      summ $OUT/prod_*.log $OUT/ll_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
