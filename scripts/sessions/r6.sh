@@ -248,6 +248,31 @@ case $P in
       done
       summ $OUT/prod_*.log $OUT/ll_*.log > $OUT/summary.txt
       ;;
+  q)  # counter rows in HBM for launches beyond the LDS rows (step_kernel HBM_ROWS): the GPU suite and smoke
+      # on the new build, then the default (one 10^4-step launch) against the previous library (400-step
+      # launches), and the driver's command, interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      for i in 1 2; do
+        step new_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_def_$i 200 python -u bench.py --steps-per-launch 400 $Q
+        step new_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+      done
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_def 300 python -u bench.py --groups 125000 $Q
+      summ $OUT/new_*.log $OUT/prev_*.log $OUT/s8_*.log > $OUT/summary.txt
+      ;;
+  r)  # one 10^4-step launch (counter rows in HBM) against 400-step launches at config 4's shard sizes
+      # (10^6 / N groups), the default's 10^4 steps, interleaved
+      for g in 125000 250000 500000; do
+        for i in 1 2; do
+          step g${g}_long_$i 200 python -u bench.py --groups $g $Q
+          step g${g}_k400_$i 200 python -u bench.py --groups $g --steps-per-launch 400 $Q
+        done
+      done
+      summ $OUT/g*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
