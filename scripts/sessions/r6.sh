@@ -273,6 +273,32 @@ case $P in
       done
       summ $OUT/g*.log > $OUT/summary.txt
       ;;
+  s)  # counter rows in HBM with a per-wave LDS window (16 steps) flushed by atomics: the launch-length and
+      # parity tests, then the default (one 10^4-step launch) against the previous library (400-step
+      # launches) at 10^6 and at config 4's 1/8 shard, interleaved; the driver's command
+      L=$PWD/raft-kotlin_amd/lib
+      step pytest 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+          -k "steps_per_launch or full_size or config4 or subrange"
+      for i in 1 2; do
+        step new_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_def_$i 200 python -u bench.py --steps-per-launch 400 $Q
+        step new_s8_$i 200 python -u bench.py --groups 125000 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_s8_$i 200 python -u bench.py --groups 125000 --steps-per-launch 400 $Q
+      done
+      step new_d20 200 python -u bench.py --steps 20 --warmup 5 $Q
+      summ $OUT/new_*.log $OUT/prev_*.log > $OUT/summary.txt
+      ;;
+  t)  # the HBM-row kernel's launch length at the default: 1,000 / 2,000 / 5,000 / 10,000 steps per launch
+      # against the previous library's 400, interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      for i in 1 2; do
+        for k in 1000 2000 5000 10000; do
+          step new_k${k}_$i 200 python -u bench.py --steps-per-launch $k $Q
+        done
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_k400_$i 200 python -u bench.py --steps-per-launch 400 $Q
+      done
+      summ $OUT/new_*.log $OUT/prev_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
