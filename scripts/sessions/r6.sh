@@ -299,6 +299,22 @@ case $P in
       done
       summ $OUT/new_*.log $OUT/prev_*.log > $OUT/summary.txt
       ;;
+  u)  # priority-band re-tune on this round's kernel (RAFT_BAND_ENDS / RAFT_AGE_SHIFTS builds): b1 later
+      # band ends 600/800/930, b2 age shifts x1.5, b3 earlier ends 400/700/880, b4 age shifts /2, against
+      # production (500/750/900, 80/40/20), interleaved on the driver's command and the 1/8 shard
+      L=$PWD/raft-kotlin_amd/lib
+      for i in 1 2 3; do
+        step prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        for v in b1 b2 b3 b4; do
+          RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step ${v}_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        done
+        step prod_s8_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        for v in b1 b2 b3 b4; do
+          RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step ${v}_s8_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        done
+      done
+      summ $OUT/*_d20_*.log $OUT/*_s8_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
