@@ -221,10 +221,12 @@ def cycle_split(pmc):
 
 def grid_fill(G: int, R: int, L: int, seven: bool) -> str:
     """How the step kernel's waves (one per 64 // R groups) fill the chip: 7
-    resident waves per SIMD for the 7-wave kernels launched at most
-    STEP_K_7WG steps (abi.bench_steps_per_launch), else 6."""
+    resident waves per SIMD for the 7-wave kernels whose counter rows fit 7
+    workgroups' LDS (launches of at most STEP_K_7WG steps, or longer ones run
+    as 400-step epochs), else 6."""
     waves = -(-G // (64 // R))
-    slots = SIMDS * (7 if seven and L <= abi.BENCH_STEPS_PER_LAUNCH else 6)
+    lds6 = abi.BENCH_STEPS_PER_LAUNCH < L <= abi.LDS_MAX_STEPS_PER_LAUNCH
+    slots = SIMDS * (7 if seven and not lds6 else 6)
     if waves < slots:
         return (f"{waves} waves < the {slots} resident wave slots of one MI355X: the grid cannot fill "
                 f"the chip ({waves / slots:.0%} of the slots), so this rate is not the kernel's throughput")
@@ -650,7 +652,7 @@ def main(argv=None, result=None):
     log_cap = max(log_cap, window)                          # the window never exceeds the physLen limit
     mode = abi.MODE_TEXTBOOK if args.mode == "textbook" else abi.MODE_REFERENCE
     net = abi.step_net_of(kw)
-    spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window, net)
+    spl = args.steps_per_launch or abi.bench_steps_per_launch(R, mode, window, net, G_local, SIMDS)
     L = launch_length(args.steps, spl)                      # every timed launch has L steps
     chunk = L * max(1, args.reduce_every // L)               # steps per step_async call / all-reduce
     # launch sub-ranges: 0 = the engine's automatic choice (one on the balanced
@@ -817,7 +819,7 @@ def main(argv=None, result=None):
             "steps_per_launch": L, "launches": launches, "parallelism": f"shard-by-group x{world}",
             "subranges": nsub,
             "step_waves_per_rank": -(-G_local // (64 // R)),
-            "grid_fill": grid_fill(G_local, R, L, abi.bench_steps_per_launch(R, mode, window, net) < abi.MAX_STEPS_PER_LAUNCH),
+            "grid_fill": grid_fill(G_local, R, L, R <= 5 or (R == 7 and net == abi.NET_PART)),
             "counter_allreduce_every": ({"end": "timed_region_once", "inline": chunk,
                                          "after": "after_timed_region_diagnostic"}[args.allreduce] if coll else None),
             "collective": ({"backend": backend, "ranks": world, "forced_at_one_rank": world == 1,

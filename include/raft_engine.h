@@ -61,7 +61,7 @@ extern "C" {
 #define RAFT_LEADER    2
 
 #define RAFT_MAX_R 8
-#define RAFT_MAX_STEPS_PER_LAUNCH 512   /* steps fused into one kernel launch (LDS counter rows) */
+#define RAFT_MAX_STEPS_PER_LAUNCH 16384 /* steps fused into one kernel launch (beyond 512: epochs) */
 #define RAFT_MAX_AE_ENTRIES 8           /* textbook mode: entries one AppendEntries request carries */
 #define RAFT_MAX_SUBRANGES 4            /* launch sub-ranges (streams) of the step kernel's grid */
 
@@ -107,7 +107,10 @@ typedef struct raft_params {
     int32_t  cmd_limit;         /* 0 = unlimited, else commands per group                           */
     int32_t  steps_per_launch;  /* engine only: steps fused in one kernel launch, 0..RAFT_MAX_STEPS_PER_LAUNCH (0 = 1);
                                    results never depend on it; <= 429 lets the 7-wave kernels (R <= 5, and
-                                   R = 7 without drops) run 7 workgroups per CU (LDS), longer launches run 6 */
+                                   R = 7 without drops) run 7 workgroups per CU (LDS), up to 512 run 6; a
+                                   longer balanced launch on one sub-range in the reference mode (not a
+                                   partitions-only kernel) runs as 400-step epochs (7 per CU), any other
+                                   is cut into launches of 512 */
     int32_t  mode;              /* RAFT_MODE_* (0 = the reference)                                  */
     int32_t  log_window;        /* 0 = every physical slot is kept (log_cap slots per replica);
                                  * else a power of two W <= log_cap: only the newest W physical

@@ -44,13 +44,22 @@ COUNTER_NAMES = [
 ]
 NUM_COUNTERS = len(COUNTER_NAMES)
 COUNTER_STRIDE = 32
-MAX_STEPS_PER_LAUNCH = 512
+MAX_STEPS_PER_LAUNCH = 16384          # include/raft_engine.h RAFT_MAX_STEPS_PER_LAUNCH
+# the longest launch whose counter rows stay in LDS for the whole launch
+# (raft_engine.hip LDS_MAX_STEPS); a longer one runs as 400-step epochs when
+# its schedule is balanced on one sub-range in the reference mode (not a
+# partitions-only kernel), else the engine cuts it to this
+LDS_MAX_STEPS_PER_LAUNCH = 512
 # bench.py's launch length for the step kernels built for 7 waves per SIMD
 # (R <= 5, or R = 7 without drops; RAFT_STEP_WAVES_PER_EU in raft_engine.hip):
 # the longest that keeps 7 step workgroups per CU within the LDS (STEP_K_7WG,
 # 429 steps).  The other kernels run 6 workgroups per CU at any length and
-# take the longest launch.
+# take the longest LDS launch.
 BENCH_STEPS_PER_LAUNCH = 400
+# bench.py's launch length where the engine runs epochs: the whole default run
+# in one launch (a launch boundary costs ~36 us / sqrt(K) of the waves'
+# uneven work; an epoch boundary only waits for a workgroup's own waves)
+LONG_STEPS_PER_LAUNCH = 10_000
 
 
 # The network faults (and command harness) a step kernel is built for
@@ -84,12 +93,20 @@ def step_net_of(kw: dict) -> int:
                     cmd_limit=kw.get("cmd_limit", 0))
 
 
-def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0, net: int = NET_ALL) -> int:
-    """Default fused launch length of bench.py for a kernel variant: 400 for the
-    7-waves-per-SIMD kernels (R <= 5, or R = 7 built for partitions only; either
-    protocol mode, flat log or ring), the longest launch for the others."""
+def bench_steps_per_launch(R: int, mode: int = 0, log_window: int = 0, net: int = NET_ALL, groups: int = 0,
+                           simds: int = 1024) -> int:
+    """Default fused launch length of bench.py for a kernel variant:
+    LONG_STEPS_PER_LAUNCH where the engine runs a long launch as epochs (the
+    reference mode, one launch sub-range -- not a partitions-only kernel --
+    and a balanced schedule: more chunks of 64 // R groups than the resident
+    wave slots of `simds` SIMDs); else 400 for the 7-waves-per-SIMD kernels (R
+    <= 5, or R = 7 built for partitions only; either protocol mode, flat log or
+    ring), the longest LDS launch for the others."""
     seven = R <= 5 or (R == 7 and net == NET_PART)
-    return BENCH_STEPS_PER_LAUNCH if seven else MAX_STEPS_PER_LAUNCH
+    balanced = -(-groups // (64 // R)) > simds * (7 if seven else 6)
+    if mode == MODE_REFERENCE and net != NET_PART and balanced:
+        return LONG_STEPS_PER_LAUNCH
+    return BENCH_STEPS_PER_LAUNCH if seven else LDS_MAX_STEPS_PER_LAUNCH
 MAX_AE_ENTRIES = 8           # include/raft_engine.h RAFT_MAX_AE_ENTRIES
 C_INDEX = {n: i for i, n in enumerate(COUNTER_NAMES)}
 

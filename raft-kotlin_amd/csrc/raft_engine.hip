@@ -59,12 +59,18 @@ constexpr int STEP_WAVES = STEP_BLOCK / 64;
 constexpr int JOB_LDS_WORDS = STEP_WAVES * 64 * 4;        // step_kernel's per-wave job-word staging
 constexpr int TALLY_LDS_WORDS = STEP_WAVES * 16;          // per-wave vote-tally words (Ctx::tl, R >= 4)
 constexpr int FLAG_LDS_WORDS = STEP_WAVES;                // balanced schedule: a wave's head piece is stored
-constexpr int PLAN_LDS_WORDS = STEP_WAVES * 8;            // each wave's plan (plan_of) and priority band
+constexpr int PLAN_LDS_WORDS = STEP_WAVES * 16;           // each wave's plans (plan_of) and priority band
 constexpr int PRE_CNT_LDS_WORDS = JOB_LDS_WORDS + TALLY_LDS_WORDS + FLAG_LDS_WORDS + PLAN_LDS_WORDS;
 // the longest launch whose LDS (job rows, tally words, K counter rows) still
 // lets 7 step workgroups share a CU's 160 KB
 constexpr int STEP_K_7WG = (160 * 1024 / 7 / 4 - PRE_CNT_LDS_WORDS) / NCW;
-static_assert(STEP_K_7WG >= 400, "bench.py's launch length (abi.BENCH_STEPS_PER_LAUNCH) keeps 7 workgroups per CU");
+static_assert(STEP_K_7WG >= 400, "a 400-step launch (or epoch) keeps 7 workgroups per CU");
+// the longest launch without epochs (its counter rows in LDS; 6 workgroups per
+// CU beyond STEP_K_7WG); a longer balanced launch on one sub-range runs as
+// epochs of EPOCH_STEPS, any other is cut into launches of LDS_MAX_STEPS
+constexpr int LDS_MAX_STEPS = 512;
+constexpr int EPOCH_STEPS = 400;
+constexpr uint32_t PART_STALE = 0x80000000u;   // Ctx::part of a piece's entry: its first step draws the window's mask
 
 
 // ---------------------------------------------------------------------------
@@ -354,7 +360,10 @@ __device__ __forceinline__ void enter_piece(Ctx<R>& c, Node& n, int wid) {
     __builtin_amdgcn_s_waitcnt(0x0F70);                                   // vmcnt(0)
 }
 
-template <int R, bool TB, bool RING, int NET>
+// EPOCHS: the kernel of a launch run as epochs (a separate instantiation, so
+// that the others carry none of its code: its epoch boundary in the step loop
+// costs the register allocation 2 VGPRs)
+template <int R, bool TB, bool RING, int NET, bool EPOCHS = false>
 __global__ __launch_bounds__(STEP_BLOCK) __attribute__((amdgpu_waves_per_eu(RAFT_STEP_WAVES_PER_EU(R, TB, RING, NET))))
 void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     using L = Lanes<R>;
@@ -373,7 +382,16 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
 #ifdef RAFT_WAVE_TIMES
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
+    // A balanced launch longer than the LDS rows hold runs as epochs of
+    // `epoch` steps: each epoch is the schedule of a launch of that length
+    // (the same chunks, McNaughton split, hand-off and priority bands), and
+    // at its end the workgroup's waves meet at a barrier, copy the epoch's
+    // counter rows to the partials and zero them.  Only the workgroup's four
+    // waves wait for each other there (their SIMDs issue other workgroups'
+    // waves meanwhile), where a launch boundary waits for every wave of the
+    // chip.
+    const int elen = EPOCHS && p.epoch > 0 && p.epoch < nsteps ? p.epoch : nsteps;
+    for (int q = threadIdx.x; q < elen * NCW; q += STEP_BLOCK) lds_cnt[q] = 0u;
     if (threadIdx.x < FLAG_LDS_WORDS) lds_flag[threadIdx.x] = 0u;
     __syncthreads();                                                      // counter rows and flags zeroed
 
@@ -399,24 +417,35 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
     // step loop made the compiler hoist and duplicate: 76 B of scratch and
     // +600 static VALU at R = 5.)
     int pc = 0;                                    // this wave's current piece
-    int k, k1, k0;                                 // its step, the step it ends before, its first step
+    int k, k1;                                     // its step, the step it ends before
     int band_left;                                 // chunk-steps to the next priority band (balanced)
+    // steps are counted from the epoch's start (k, the pieces' k0 / k1, the
+    // counter rows); the epoch's first step is tb - t0, its first step index
+    // tb, and its length and first step sit in the wave's plan words [5], [7]
+    uint32_t tb = t0;
     {   // (a wave's first piece is never a tail: a wave runs its head first)
-        const uint4 pl = plan_of(wib, nsteps);
-        *(uint4*)(lds_plan + wib * 8) = pl;
+        const uint4 pl = plan_of(wib, elen);
+        *(uint4*)(lds_plan + wib * 16) = pl;
+        // [8..11]: the plan of a whole epoch, [12..15]: of the last one (the
+        // epoch boundary only reads them: plan_of's divisions in the step
+        // loop made the register allocation spill)
+        *(uint4*)(lds_plan + wib * 16 + 8) = pl;
+        if (EPOCHS && elen < nsteps)
+            *(uint4*)(lds_plan + wib * 16 + 12) = plan_of(wib, nsteps - (nsteps - 1) / elen * elen);
         const bool bal = kernargs()->bal_chunks != 0;
-        const uint32_t Q = plan_units(pl, nsteps);
-        // [4]: the band now, [5]: chunk-steps done at its start, [6]: Q
-        *(uint4*)(lds_plan + wib * 8 + 4) = make_uint4(3u, 0u, Q, 0u);
+        const uint32_t Q = plan_units(pl, elen);
+        // [4]: the band now, [5]: the epoch's length, [6]: Q, [7]: its first step
+        *(uint4*)(lds_plan + wib * 16 + 4) = make_uint4(3u, (uint32_t)elen, Q, 0u);
         band_left = bal ? (int)band_end<SLOTS>(Q, 3) : 0x7FFFFFFF;
         if (bal) set_priority(3);
-        const Piece pz = piece_of(pl, 0, nsteps);
+        const Piece pz = piece_of(pl, 0, elen);
         enter_piece<R, RING>(c, n, piece_chunk(pz.chunk));
-        k = k0 = pz.k0;
+        k = pz.k0;
+        c.part = PART_STALE;
         k1 = pz.k1;
     }
     for (;;) {
-        const uint32_t t = t0 + (uint32_t)k;
+        const uint32_t t = tb + (uint32_t)k;
         c.t = t;
         // The lane geometry (r, base) is carried across steps behind an opaque
         // copy: otherwise the optimiser hoists dozens of loop-invariant lane
@@ -437,7 +466,8 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             if (pperiod > 0) {                                            // S-11 partitions
                 const uint32_t ph = t % (uint32_t)pperiod;
                 if ((int64_t)ph < kp->part_len) {
-                    if (k == k0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
+                    // (a piece enters with c.part = PART_STALE: its first step in a window draws)
+                    if ((int32_t)c.part < 0 || ph == 0) c.part = kdraw(p, t - ph, c.gid(), RAFT_RNG_PARTITION, 0).x & L::ALL;
                 } else {
                     c.part = 0;
                 }
@@ -459,12 +489,12 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         c.clk.mark(PH_CNT);
         if (RARE(--band_left == 0)) {              // this wave's next priority band (balanced)
             const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
-            uint4 bs = *(const uint4*)(lds_plan + wb * 8 + 4);
+            uint4 bs = *(const uint4*)(lds_plan + wb * 16 + 4);
             const int b = __builtin_amdgcn_readfirstlane((int)bs.x) - 1;
             const uint32_t Q = __builtin_amdgcn_readfirstlane(bs.z);
             set_priority(b);
             band_left = b > 0 ? (int)(band_end<SLOTS>(Q, b) - band_end<SLOTS>(Q, b + 1)) : 0x7FFFFFFF;
-            *(lds_plan + wb * 8 + 4) = (uint32_t)b;
+            *(lds_plan + wb * 16 + 4) = (uint32_t)b;
         }
         if (++k == k1) {                           // the piece ends: store its chunk (rare)
             if (c.live) {
@@ -476,7 +506,7 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
             // this wave's index from its job rows' address (kept live across
             // the loop, the index would pin a register)
             const int wb = __builtin_amdgcn_readfirstlane((int)((c.jl - lds) >> 8));
-            uint4 pl = *(const uint4*)(lds_plan + wb * 8);
+            uint4 pl = *(const uint4*)(lds_plan + wb * 16);
             pl.x = __builtin_amdgcn_readfirstlane(pl.x);        // one word for the whole wave
             pl.y = __builtin_amdgcn_readfirstlane(pl.y);
             pl.z = __builtin_amdgcn_readfirstlane(pl.z);
@@ -485,11 +515,55 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(lds_flag + wb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (++pc == n_pieces(pl)) break;
-            const Piece pz = piece_of(pl, pc, nsteps);
+            if (++pc == n_pieces(pl)) {
+                if constexpr (!EPOCHS) break;
+                const uint32_t ke = __builtin_amdgcn_readfirstlane(lds_plan[wb * 16 + 5]);
+                const uint32_t kb = __builtin_amdgcn_readfirstlane(lds_plan[wb * 16 + 7]);
+                if (kb + ke >= (uint32_t)nsteps) break;
+                // the epoch ends: its rows to the partials (rows [kb, kb + ke)
+                // of the launch), zeroed for the next; the chunks' states of
+                // every wave stored (vmcnt(0) before the barrier) and this
+                // CU's vector L1 invalidated before the next epoch loads them
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                {
+                    // (the thread index behind an opaque copy: hoisted out of
+                    // the step loop, its products would pin registers there)
+                    int tid = (int)threadIdx.x;
+                    asm volatile("" : "+v"(tid));
+                    const KernArgs kp = kernargs();
+                    uint32_t* const part = kp->part + kp->part_col0 + blockIdx.x;
+                    const uint32_t stride = (uint32_t)kp->part_stride;          // partials < 2^32 words
+                    for (int q = tid; q < (int)ke * NCW; q += STEP_BLOCK) {
+                        part[(kb * NCW + (uint32_t)q) * stride] = lds_cnt[q];
+                        lds_cnt[q] = 0u;
+                    }
+                    if (tid < FLAG_LDS_WORDS) lds_flag[tid] = 0u;
+                }
+                __syncthreads();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                asm volatile("buffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t kb2 = kb + ke;
+                const int ke2 = min(kernargs()->epoch, nsteps - (int)kb2);
+                tb += ke;
+                pl = *(const uint4*)(lds_plan + wb * 16 + (ke2 == kernargs()->epoch ? 8 : 12));
+                pl.x = __builtin_amdgcn_readfirstlane(pl.x);
+                pl.y = __builtin_amdgcn_readfirstlane(pl.y);
+                pl.z = __builtin_amdgcn_readfirstlane(pl.z);
+                pl.w = __builtin_amdgcn_readfirstlane(pl.w);
+                *(uint4*)(lds_plan + wb * 16) = pl;
+                const uint32_t Q = plan_units(pl, ke2);
+                *(uint4*)(lds_plan + wb * 16 + 4) = make_uint4(3u, (uint32_t)ke2, Q, kb2);
+                band_left = (int)band_end<SLOTS>(Q, 3);
+                set_priority(3);
+                pc = 0;
+            }
+            const int kel = EPOCHS ? (int)__builtin_amdgcn_readfirstlane(lds_plan[wb * 16 + 5]) : nsteps;
+            const Piece pz = piece_of(pl, pc, kel);
             if (pz.wait) wait_head(lds_flag + wb - 1);
             enter_piece<R, RING>(c, n, piece_chunk(pz.chunk));
-            k = k0 = pz.k0;
+            k = pz.k0;
+            c.part = PART_STALE;
             k1 = pz.k1;
         }
     }
@@ -520,7 +594,8 @@ void step_kernel(DevParams p, uint32_t t0, int nsteps) {
         const KernArgs kp = kernargs();
         uint32_t* const part = kp->part + kp->part_col0 + blockIdx.x;
         const int64_t stride = kp->part_stride;
-        for (int q = threadIdx.x; q < nsteps * NCW; q += STEP_BLOCK) part[(int64_t)q * stride] = lds_cnt[q];
+        const int ke = EPOCHS ? (int)lds_plan[5] : nsteps, kb = EPOCHS ? (int)lds_plan[7] : 0;   // (the last epoch)
+        for (int q = threadIdx.x; q < ke * NCW; q += STEP_BLOCK) part[((int64_t)kb * NCW + q) * stride] = lds_cnt[q];
     }
 }
 
@@ -600,7 +675,7 @@ __global__ __launch_bounds__(BLOCK) void rebuild_cache_kernel(DevParams p) {
 // counters[k][c] = sum over the step workgroups b of the 16-bit half of
 // partials[k][][b] at COUNTER_SLOT[c] (raft_step.h), in ONE dispatch with no memset (a memset, an
 // atomic-add reduction and their two dependent dispatch gaps were ~6 % of a
-// 20-step run).  Grid (chunks, nsteps * NCW): each workgroup sums both halves
+// 20-step run).  Grid chunks x nsteps * NCW: each workgroup sums both halves
 // of one packed counter word over a chunk of REDUCE_CHUNK partials (each word
 // is read once) and adds each half, with a ticket of 1 << 48, into that
 // counter's 64-bit accumulator (one returning atomic, no fence: a
@@ -629,13 +704,16 @@ __device__ __forceinline__ void reduce_emit(int64_t* row, int c, unsigned long l
 }
 // APPEND_SKIPPED is derived per workgroup partial as R * SESSIONS_TICKED -
 // APPEND_SENT (the step kernel does not count it, see Stepper::tick).
+// Grid: nch chunks x (K * NCW) words, flattened (a launch of 10^4 steps has
+// more words than a grid dimension of 2^16).
 __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* __restrict__ partials, int nparts,
-                                                                int R, int64_t* __restrict__ counters,
+                                                                int nch_, int R, int64_t* __restrict__ counters,
                                                                 unsigned long long* __restrict__ accum) {
     __shared__ uint32_t acc[2][WAVES_PER_BLOCK];
-    const int k = blockIdx.y / NCW, w = blockIdx.y % NCW;
+    const int kw = (int)(blockIdx.x / (unsigned)nch_), chunk = (int)(blockIdx.x - (unsigned)kw * (unsigned)nch_);
+    const int k = kw / NCW, w = kw % NCW;
     const int c0 = counter_of_slot(2 * w), c1 = counter_of_slot(2 * w + 1);   // -1: an unused slot
-    const int b0 = blockIdx.x * REDUCE_CHUNK;
+    const int b0 = chunk * REDUCE_CHUNK;
     constexpr int SK = RAFT_C_APPEND_SKIPPED;
     constexpr int TK = RAFT_C_SESSIONS_TICKED, SN = RAFT_C_APPEND_SENT;
     uint32_t lo = 0, hi = 0;        // < 2^19 * 16 per thread
@@ -659,14 +737,14 @@ __global__ __launch_bounds__(BLOCK) void reduce_counters_kernel(const uint32_t* 
     }
     __syncthreads();
     int64_t* row = counters + (int64_t)k * RAFT_COUNTER_STRIDE;
-    if (w == 0 && blockIdx.x == 0 && threadIdx.x >= NC && threadIdx.x < RAFT_COUNTER_STRIDE) row[threadIdx.x] = 0;
+    if (w == 0 && chunk == 0 && threadIdx.x >= NC && threadIdx.x < RAFT_COUNTER_STRIDE) row[threadIdx.x] = 0;
     if (threadIdx.x != 0) return;
     unsigned long long sl = 0, sh = 0;
     for (int q = 0; q < WAVES_PER_BLOCK; ++q) {
         sl += acc[0][q];
         sh += acc[1][q];
     }
-    const unsigned long long nch = gridDim.x;
+    const unsigned long long nch = (unsigned long long)nch_;
     if (c0 >= 0) reduce_emit(row, c0, sl, nch, &accum[(int64_t)k * NC + c0]);
     if (c1 >= 0) reduce_emit(row, c1, sh, nch, &accum[(int64_t)k * NC + c1]);
 }
@@ -890,20 +968,37 @@ static StepKernel step_fn(const DevParams& d, const raft_params& p, bool iso) {
     }
     return step_kernel<R, TB, RING, NET_ALL>;
 }
+// the epochs kernels: the reference mode's drops + churn kernel (config 3 and
+// its shards) and the general kernel; a launch of another is cut (nullptr)
+template <int R, bool RING>
+static StepKernel step_fn_epochs(const DevParams& d, const raft_params& p, bool iso) {
+    if (p.kernel == RAFT_KERNEL_GENERAL) return step_kernel<R, false, RING, NET_ALL, true>;
+    if constexpr (R == 3 || R == 5 || R == 7) {
+        const int net = step_net(d, p, R, iso);
+        if (net == (NET_DROP | NET_ISO | NET_CMDLOW)) return step_kernel<R, false, RING, NET_DROP | NET_ISO | NET_CMDLOW, true>;
+        if (net == NET_PART) return nullptr;
+    }
+    return step_kernel<R, false, RING, NET_ALL, true>;
+}
 template <int R> struct KernL {
-    static void run(raft_engine* e, StepKernel* out) {
+    static void run(raft_engine* e, bool epochs, StepKernel* out) {
         // a flat log (log_window 0) keeps every slot: the kernel without window checks
         const bool iso = e->dp.churn_thr32 != 0 || e->iso_written;
-        *out = e->p.mode == RAFT_MODE_TEXTBOOK
-                   ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p, iso)
-                                      : step_fn<R, true, false>(e->dp, e->p, iso))
-                   : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p, iso)
-                                      : step_fn<R, false, false>(e->dp, e->p, iso));
+        if (epochs)
+            *out = e->p.mode == RAFT_MODE_TEXTBOOK ? nullptr
+                   : (e->p.log_window ? step_fn_epochs<R, true>(e->dp, e->p, iso)
+                                      : step_fn_epochs<R, false>(e->dp, e->p, iso));
+        else
+            *out = e->p.mode == RAFT_MODE_TEXTBOOK
+                       ? (e->p.log_window ? step_fn<R, true, true>(e->dp, e->p, iso)
+                                          : step_fn<R, true, false>(e->dp, e->p, iso))
+                       : (e->p.log_window ? step_fn<R, false, true>(e->dp, e->p, iso)
+                                          : step_fn<R, false, false>(e->dp, e->p, iso));
     }
 };
-static StepKernel step_kernel_of(raft_engine* e) {
+static StepKernel step_kernel_of(raft_engine* e, bool epochs = false) {
     StepKernel k = nullptr;
-    dispatch_R<KernL>(e->p.R, e, &k);
+    dispatch_R<KernL>(e->p.R, e, epochs, &k);
     return k;
 }
 static size_t step_lds_bytes(int k) { return (size_t)(PRE_CNT_LDS_WORDS + k * NCW) * 4; }
@@ -915,9 +1010,10 @@ static size_t step_lds_bytes(int k) { return (size_t)(PRE_CNT_LDS_WORDS + k * NC
 struct LaunchGeo {
     int w0[RAFT_MAX_SUBRANGES + 1], nb[RAFT_MAX_SUBRANGES], col0[RAFT_MAX_SUBRANGES], bal[RAFT_MAX_SUBRANGES];
     int stride, resident, balanced;
+    int epoch;                    // steps per epoch (0: one epoch)
 };
-static int launch_geo(raft_engine* e, StepKernel kern, int k, LaunchGeo& geo) {
-    const size_t lds = step_lds_bytes(k);
+static int launch_geo(raft_engine* e, StepKernel kern, int k, int epoch, LaunchGeo& geo) {
+    const size_t lds = step_lds_bytes(epoch > 0 ? std::min(k, epoch) : k);
     // workgroups per CU, cached per (kernel, LDS bytes): a run alternates a
     // few launch lengths (warmup, timed, a remainder), and the query costs
     // ~1 us of host time ahead of the launch
@@ -932,6 +1028,7 @@ static int launch_geo(raft_engine* e, StepKernel kern, int k, LaunchGeo& geo) {
         e->occ_lds[slot] = lds;
         e->occ_wg[slot] = std::max(1, wg);
     }
+    geo.epoch = epoch;
     geo.resident = e->occ_wg[slot] * e->ncu;
     const int cap = std::max(1, (e->sched_wg > 0 ? std::min(e->sched_wg, geo.resident) : geo.resident) / e->nsub);
     geo.stride = 0;
@@ -950,7 +1047,8 @@ static int launch_geo(raft_engine* e, StepKernel kern, int k, LaunchGeo& geo) {
         geo.nb[q] = bal ? std::min(cap, n / STEP_WAVES) : e->sub_b0[q + 1] - e->sub_b0[q];
         // plan_of's 32-bit arithmetic: (wave + 1) * m * K < 2^32 for a
         // workgroup's m = ceil(n / nb) chunks
-        if (bal && (uint64_t)STEP_WAVES * (uint64_t)((n + geo.nb[q] - 1) / geo.nb[q]) * (uint64_t)k >= (1ull << 32))
+        const int kp_ = epoch > 0 ? std::min(k, epoch) : k;                // a plan spans one epoch
+        if (bal && (uint64_t)STEP_WAVES * (uint64_t)((n + geo.nb[q] - 1) / geo.nb[q]) * (uint64_t)kp_ >= (1ull << 32))
             return fail(RAFT_EINVAL, "balanced launch too long for its workgroups (4 * chunks per workgroup * "
                                      "steps_per_launch >= 2^32): raise schedule_workgroups or lower steps_per_launch");
         geo.col0[q] = geo.stride;
@@ -973,8 +1071,10 @@ template <int R> struct StepL {
         d.bal_rem = geo.bal[q] % geo.nb[q];
         d.part_col0 = geo.col0[q];
         d.part_stride = geo.stride;
-        hipExtLaunchKernelGGL(kern, dim3(geo.nb[q]), dim3(STEP_BLOCK), (uint32_t)step_lds_bytes(k), st, ev0, ev1, 0u, d,
-                              t0, k);
+        d.epoch = geo.epoch;
+        hipExtLaunchKernelGGL(kern, dim3(geo.nb[q]), dim3(STEP_BLOCK),
+                              (uint32_t)step_lds_bytes(geo.epoch > 0 ? std::min(k, geo.epoch) : k), st, ev0, ev1, 0u,
+                              d, t0, k);
     }
 };
 template <int R> struct PackL {
@@ -1107,6 +1207,8 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     e->bflags_host = nullptr;
     e->aux = nullptr;
     e->aux_bytes = 0;
+    e->hpart = nullptr;
+    e->hpart_bytes = 0;
     e->device = device;
     e->t = 0;
     const int64_t G = p->G, R = p->R;
@@ -1154,7 +1256,7 @@ int raft_engine_create(const raft_params* p, int device, raft_engine** out) {
     const size_t log_b = (size_t)log_waves * nslots * 64 * 8;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     // sized for the largest launch, so steps_per_launch can change later
-    const size_t part_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NCW * e->nblocks * 4;
+    const size_t part_b = (size_t)LDS_MAX_STEPS * NCW * e->nblocks * 4;
     const size_t cnt_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * RAFT_COUNTER_STRIDE * 8;
     const size_t acc_b = (size_t)RAFT_MAX_STEPS_PER_LAUNCH * NC * 8;
     e->bytes = al(st_b) + al(spill_b) + al(gx_b) + 2 * al(part_b) + al(cnt_b) + al(acc_b) + al(log_b);
@@ -1270,6 +1372,7 @@ int raft_engine_destroy(raft_engine* e) {
     if (e->hst) (void)hipHostFree(e->hst);
     if (e->bflags_host) (void)hipHostFree(e->bflags_host);
     if (e->aux) (void)hipFree(e->aux);
+    if (e->hpart) (void)hipFree(e->hpart);
     (void)hipFree(e->base);
     (void)hipStreamDestroy(e->stream);
     delete e;
@@ -1279,6 +1382,7 @@ int raft_engine_destroy(raft_engine* e) {
 // Grow the timing-event pool to hold `pairs` more launches.  Called when
 // timing is switched on, so a timed region never creates events (64
 // hipEventCreate calls cost ~0.1 ms of host time, 7 % of a 20-step run).
+static int grow_dev(raft_engine* e, char** buf, size_t* have, size_t need);
 static int reserve_events(raft_engine* e, size_t pairs) {
     while (e->ev_used + 2 * pairs > e->ev.size()) {
         hipEvent_t x;
@@ -1314,12 +1418,28 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
         e->fork_needed = false;
     }
     const StepKernel kern = n_steps > 0 ? step_kernel_of(e) : nullptr;
+    const StepKernel kern_ep = n_steps > 0 && !split && e->K > LDS_MAX_STEPS ? step_kernel_of(e, true) : nullptr;
     for (int32_t done = 0; done < n_steps;) {
-        const int k = std::min<int32_t>(e->K, n_steps - done);
+        int k = std::min<int32_t>(e->K, n_steps - done);
         const int buf = split ? (int)(e->launches_issued & 1) : 0;
         uint32_t* part = buf ? e->partials2 : e->partials;
         LaunchGeo geo;
-        if (int rc = launch_geo(e, kern, k, geo)) return rc;
+        // a launch beyond LDS_MAX_STEPS: epochs when balanced on one
+        // sub-range (its partials [k][NCW][workgroups] in a grow-only
+        // buffer), else cut to LDS_MAX_STEPS
+        bool epochs = false;
+        if (k > LDS_MAX_STEPS && kern_ep) {
+            if (int rc = launch_geo(e, kern_ep, k, EPOCH_STEPS, geo)) return rc;
+            epochs = geo.balanced == 1;
+        }
+        if (epochs) {
+            const size_t need = (size_t)k * NCW * (size_t)geo.stride * 4;
+            if (int rc = grow_dev(e, (char**)&e->hpart, &e->hpart_bytes, need)) return rc;
+            part = e->hpart;
+        } else {
+            k = std::min(k, LDS_MAX_STEPS);
+            if (int rc = launch_geo(e, kern, k, 0, geo)) return rc;
+        }
         if (e->timing && e->ev_used + 2 * e->nsub > e->ev.size())
             if (int rc = reserve_events(e, 64 + e->nsub)) return rc;
         for (int q = 0; q < e->nsub; ++q) {
@@ -1331,7 +1451,8 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
             }
             hipStream_t st = split ? e->sub_stream[q] : e->stream;
             if (split && e->launches_issued >= 2) HIP_TRY(hipStreamWaitEvent(st, e->ev_red_done[buf], 0));
-            dispatch_R<StepL>(e->p.R, e, kern, (uint32_t)(e->t + done), k, ev0, ev1, st, geo, q, part);
+            dispatch_R<StepL>(e->p.R, e, epochs ? kern_ep : kern, (uint32_t)(e->t + done), k, ev0, ev1, st, geo, q,
+                              part);
             if (split) {
                 HIP_TRY(hipEventRecord(e->ev_sub_done[q], st));
                 HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_sub_done[q], 0));
@@ -1349,8 +1470,9 @@ int raft_engine_step_async(raft_engine* e, int32_t n_steps, int64_t* counters_de
         e->last.balanced = geo.balanced;
         e->last.subranges = e->nsub;
         int64_t* dst = counters_dev ? counters_dev + (int64_t)done * RAFT_COUNTER_STRIDE : e->counters_dev;
-        const dim3 rg((unsigned)((geo.stride + REDUCE_CHUNK - 1) / REDUCE_CHUNK), (unsigned)(k * NCW));
-        reduce_counters_kernel<<<rg, BLOCK, 0, e->stream>>>(part, geo.stride, e->p.R, dst, e->accum);
+        const int nch = (geo.stride + REDUCE_CHUNK - 1) / REDUCE_CHUNK;
+        reduce_counters_kernel<<<(unsigned)(nch * k * NCW), BLOCK, 0, e->stream>>>(part, geo.stride, nch, e->p.R, dst,
+                                                                                  e->accum);
         if (split) HIP_TRY(hipEventRecord(e->ev_red_done[buf], e->stream));
         ++e->launches_issued;
         done += k;
@@ -1541,7 +1663,7 @@ int raft_engine_set_step_index(raft_engine* e, int64_t t) {
     return RAFT_OK;
 }
 int64_t raft_engine_device_bytes(raft_engine* e) {
-    return e ? (int64_t)(e->bytes + e->bst_bytes + e->bio_bytes + e->aux_bytes) : -1;
+    return e ? (int64_t)(e->bytes + e->bst_bytes + e->bio_bytes + e->aux_bytes + e->hpart_bytes) : -1;
 }
 int raft_engine_trim_staging(raft_engine* e) {
     if (!e) return fail(RAFT_EINVAL, "null engine");

@@ -73,6 +73,8 @@ struct raft_engine {
     uint32_t occ_next;
     uint32_t* partials;         // [K][NCW][nblocks] packed per-workgroup counter partials (buffer 0)
     uint32_t* partials2;        // buffer 1: launches alternate between the two when nsub > 1
+    uint32_t* hpart;            // [K][NCW][workgroups] partials of a launch run as epochs (grow-only,
+    size_t hpart_bytes;         // raft_engine_step_async)
     // launch sub-ranges (raft_engine_step_async): the step workgroups split
     // into nsub contiguous ranges, each launched on its own stream, so one
     // range's last waves overlap another's next launch instead of leaving

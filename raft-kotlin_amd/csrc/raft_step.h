@@ -142,6 +142,7 @@ struct DevParams {
     uint32_t* part;
     int32_t wave0, part_col0, part_stride;
     int32_t bal_chunks, bal_q, bal_rem;        // (bal_q, bal_rem) = bal_chunks / and % the workgroups
+    int32_t epoch;                             // balanced: steps per epoch of a longer launch (0: one epoch)
     uint32_t* status;                          // engine status word (page-locked host): RAFT_DEV_* bits
 };
 constexpr uint32_t RAFT_DEV_WAIT_TIMEOUT = 1u;  // a balanced-schedule wave gave up waiting for its head piece

@@ -342,8 +342,7 @@ def side_leg(args, kw, mode, world, rank, local, dev, coll, log_cap, L, chunk, s
            "ms_per_step": leg["elapsed"] * 1e3 / args.steps, "groups_total": total, "groups_per_rank": per_rank,
            "steps_per_launch": L, "subranges": nsub, "log_window": window,
            "step_waves_per_rank": -(-G // (64 // R)),
-           "grid_fill": grid_fill(G, R, L, abi.bench_steps_per_launch(R, mode, window, abi.step_net_of(kw))
-                                < abi.MAX_STEPS_PER_LAUNCH),
+           "grid_fill": grid_fill(G, R, L, R <= 5 or (R == 7 and abi.step_net_of(kw) == abi.NET_PART)),
            "kernel_avg_ms_per_rank": leg["kern_avg_per_rank"],
            "timing": {"wall_ms": leg["wall"] * 1e3, "stream_event_ms": leg["ev_ms"],
                       "step_kernel_ms_total": leg["kern_ms"], "allreduce_ms": leg["allreduce_ms"]},

@@ -315,6 +315,38 @@ case $P in
       done
       summ $OUT/*_d20_*.log $OUT/*_s8_*.log > $OUT/summary.txt
       ;;
+  v)  # long launches as 400-step epochs (a workgroup barrier per epoch instead of a chip-wide launch
+      # boundary): the launch-length / full-size parity tests, then the default (one 10^4-step launch)
+      # against the previous library (400-step launches) at 10^6 and at config 4's shard sizes, interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      step pytest 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+          -k "steps_per_launch or full_size or config4 or subrange"
+      for i in 1 2; do
+        for g in 1000000 125000 250000; do
+          step new_g${g}_$i 200 python -u bench.py --groups $g $Q
+          RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_g${g}_$i 200 python -u bench.py --groups $g --steps-per-launch 400 $Q
+        done
+      done
+      step new_d20 200 python -u bench.py --steps 20 --warmup 5 $Q
+      summ $OUT/new_*.log $OUT/prev_*.log > $OUT/summary.txt
+      ;;
+  w)  # the epochs build as the product (a separate kernel instantiation for epochs): the GPU suite and
+      # smoke, then the driver's command (no epochs: must equal production) and the default / the 1/8
+      # shard (one 10^4-step launch of epochs) against the previous library, interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      for i in 1 2 3; do
+        step new_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+      done
+      for i in 1 2; do
+        step new_def_$i 200 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_def_$i 200 python -u bench.py --steps-per-launch 400 $Q
+      done
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step new_s8 200 python -u bench.py --groups 125000 $Q
+      summ $OUT/new_*.log $OUT/prev_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0

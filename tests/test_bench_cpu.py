@@ -104,7 +104,16 @@ def test_default_launch_length_per_kernel_variant():
     take the longest launch (raft_engine.hip RAFT_STEP_WAVES_PER_EU)."""
     assert abi.bench_steps_per_launch(5) == abi.BENCH_STEPS_PER_LAUNCH == 400
     assert abi.bench_steps_per_launch(3) == 400
-    assert abi.bench_steps_per_launch(7) == abi.MAX_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(7) == abi.LDS_MAX_STEPS_PER_LAUNCH
+    # epochs: the reference mode on a balanced schedule (more chunks than
+    # resident wave slots) and one sub-range launches the whole default run
+    net3 = abi.step_net_of(abi.CONFIGS[3])
+    assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 0, net3, 10**6) == abi.LONG_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 256, net3, 125_000) == abi.LONG_STEPS_PER_LAUNCH
+    assert abi.bench_steps_per_launch(5, abi.MODE_REFERENCE, 0, net3, 10**4) == 400          # one chunk per wave
+    assert abi.bench_steps_per_launch(5, abi.MODE_TEXTBOOK, 0, net3, 10**6) == 400          # no epochs kernel
+    assert abi.bench_steps_per_launch(7, abi.MODE_REFERENCE, 0, abi.NET_PART, 10**6) == 400   # sub-ranges
+    assert abi.LONG_STEPS_PER_LAUNCH <= abi.MAX_STEPS_PER_LAUNCH
     # config 5 (R = 7, partitions, no drops) runs the 7-wave partitions-only kernel
     net5 = abi.step_net_of(abi.CONFIGS[5])
     assert net5 == abi.NET_PART and abi.bench_steps_per_launch(7, abi.MODE_REFERENCE, 0, net5) == 400

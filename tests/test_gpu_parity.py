@@ -206,9 +206,20 @@ def test_steps_per_launch_invariance():
     digests = []
     # 600 = one full 512-step launch + 88; 433 / 434: the longest launch at 7
     # workgroups per CU and the shortest at 6 (STEP_K_7WG, raft_engine.hip)
-    for k in (1, 7, 32, 128, abi.BENCH_STEPS_PER_LAUNCH, 433, 434, abi.MAX_STEPS_PER_LAUNCH):
+    for k in (1, 7, 32, 128, abi.BENCH_STEPS_PER_LAUNCH, 433, 434, abi.LDS_MAX_STEPS_PER_LAUNCH, 600):
         e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=k, **kw))
         c = e.step(600)
+        # one chunk per wave: a launch beyond the LDS rows is cut to 512 steps
+        assert e.kernel_info()["steps"] == (88 if k == 600 else 600 % k or k)
+        digests.append((e.digest(), c.tobytes()))
+    # the balanced schedule (forced at this size): 450 steps per launch (LDS
+    # rows, 6 workgroups per CU), 600 and 1,000 (one launch of 400-step epochs
+    # and a shorter last one)
+    for k in (450, 600, 1000):
+        e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=k, schedule=abi.SCHED_BALANCED, **kw))
+        c = e.step(600)
+        info = e.kernel_info()
+        assert info["balanced"] == 1 and info["steps"] == (600 % k or k)
         digests.append((e.digest(), c.tobytes()))
     # steps_per_launch changed mid-run (bench.py's streaming leg)
     e = RaftEngine(abi.make_params(log_cap=400, steps_per_launch=64, **kw))
@@ -527,9 +538,12 @@ ONE, BAL = abi.SCHED_ONE_PER_WAVE, abi.SCHED_BALANCED
 FULL_SIZE_CASES = [
     (3, 0, 1), (3, 0, 20, 1), (3, 0, 20, 1, ONE), (3, 0, abi.BENCH_STEPS_PER_LAUNCH),
     (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (3, 0, abi.BENCH_STEPS_PER_LAUNCH, 3, ONE),
-    (3, 256, 1), (3, 256, abi.BENCH_STEPS_PER_LAUNCH), (3, 256, abi.MAX_STEPS_PER_LAUNCH),
-    (5, 0, 1), (5, 0, abi.BENCH_STEPS_PER_LAUNCH), (5, 0, 500), (5, 0, abi.MAX_STEPS_PER_LAUNCH),
+    (3, 256, 1), (3, 256, abi.BENCH_STEPS_PER_LAUNCH), (3, 256, abi.LDS_MAX_STEPS_PER_LAUNCH),
+    (5, 0, 1), (5, 0, abi.BENCH_STEPS_PER_LAUNCH), (5, 0, 500), (5, 0, abi.LDS_MAX_STEPS_PER_LAUNCH),
     (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 3), (5, 0, 500, 4, ONE), (5, 0, abi.BENCH_STEPS_PER_LAUNCH, 1, BAL),
+    # the bench default's one 10^4-step launch (25 epochs of 400 steps); the
+    # ring the same way; config 5's sub-ranges cut it to 512-step launches
+    (3, 0, abi.LONG_STEPS_PER_LAUNCH), (3, 256, abi.LONG_STEPS_PER_LAUNCH), (5, 0, abi.LONG_STEPS_PER_LAUNCH),
 ]
 
 
@@ -548,9 +562,10 @@ def test_full_size_digest(case):
     group) and its per-step counters, precomputed on the CPU by
     tests/golden/make_full_size.py.  For config 3 the flat-log cases are the
     exact kernel bench.py times (the digest over every physical slot,
-    `digest_full_log`), at the driver's launch length (20), the bench
-    default (400) and one step per launch; the ring cases check the 256-slot
-    window (`digest`: the retained slots only)."""
+    `digest_full_log`), at the driver's launch length (20), 400, the bench
+    default (one 10^4-step launch of 400-step epochs) and one step per
+    launch; the ring cases check the 256-slot window (`digest`: the retained
+    slots only)."""
     import json
     cfg, window, spl = case[:3]
     nsub = case[3] if len(case) > 3 else 0
@@ -587,7 +602,8 @@ def test_config4_strong_split_full_size(n):
     split into n contiguous global-id shards (bench.shard, "strong": the
     ranks of `bench.py --gpus n`), each its own engine at its global offset
     g0, created and closed in turn, for 10^4 steps -- at the driver's launch
-    (20 steps, one sub-range) and at the bench default (400).  The summed
+    (20 steps, one sub-range), at 400 and in one 10^4-step launch (epochs).
+    The summed
     per-step counter rows equal the oracle's for the whole 10^6 groups
     (full_size_counters.npz) and the digests sum (mod 2^64) to its whole-run
     digest over every physical slot (the digest is a sum over groups)."""
@@ -596,7 +612,7 @@ def test_config4_strong_split_full_size(n):
     meta = json.load(open(FULL))["c3"]
     want = np.load(os.path.join(os.path.dirname(FULL), "full_size_counters.npz"))["c3_counters"]
     kw = dict(abi.CONFIGS[3])
-    for spl in (20, abi.BENCH_STEPS_PER_LAUNCH):
+    for spl in (20, abi.BENCH_STEPS_PER_LAUNCH, abi.LONG_STEPS_PER_LAUNCH):
         total = np.zeros_like(want)
         dsum = 0
         for rank in range(n):
