@@ -347,6 +347,28 @@ case $P in
       RAFT_BENCH_FORCE_COLLECTIVE=1 step new_s8 200 python -u bench.py --groups 125000 $Q
       summ $OUT/new_*.log $OUT/prev_*.log > $OUT/summary.txt
       ;;
+  x)  # PMC rows of the epochs build (kernel and batch sources changed): both bench commands, the 1/8
+      # shard's and the handler batches'; merged back here into profiles/pmc_rows.json / pmc_handler.json
+      TAG=r6_ep_d20 ARGS="--steps 20 --warmup 5" step pmc_d20 900 bash scripts/pmc_bench.sh
+      TAG=r6_ep_def ARGS="" step pmc_def 900 bash scripts/pmc_bench.sh
+      TAG=r6_ep_s8 ARGS="--groups 125000 --steps 20 --warmup 5" step pmc_s8 900 bash scripts/pmc_bench.sh
+      TAG=r6_ep step pmch 900 bash scripts/pmc_handler.sh
+      ;;
+  y)  # short balanced launches as epochs too (RAFT_SHORT_EPOCH=E: a launch of more than E steps runs
+      # E-step epochs, so every wave's share covers each step range equally -- the election storm's
+      # heavy steps and the quiet ones): parity of the launch-length / full-size / config-4 tests at
+      # E = 5, then the driver's command and the 1/8 shard at E = 0 / 5 / 10, interleaved
+      RAFT_SHORT_EPOCH=5 step pytest 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 \
+          --timeout-method thread -k "steps_per_launch or full_size or config4"
+      for i in 1 2 3; do
+        for E in 0 5 10; do
+          RAFT_SHORT_EPOCH=$E step d20_e${E}_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+          RAFT_SHORT_EPOCH=$E RAFT_BENCH_FORCE_COLLECTIVE=1 \
+            step s8_e${E}_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        done
+      done
+      summ $OUT/d20_*.log $OUT/s8_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
