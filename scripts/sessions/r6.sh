@@ -369,6 +369,11 @@ case $P in
       done
       summ $OUT/d20_*.log $OUT/s8_*.log > $OUT/summary.txt
       ;;
+  z)  # per-step cost profile (scripts/step_profile.py): one-step launches from step 0 at full size and
+      # at the 1/8 shard, and a steady-state window
+      step prof_full 300 python -u scripts/step_profile.py --groups 1000000 --steps 40 --also 3000:3020
+      step prof_s8 300 python -u scripts/step_profile.py --groups 125000 --steps 40 --also 3000:3020
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
