@@ -374,6 +374,15 @@ case $P in
       step prof_full 300 python -u scripts/step_profile.py --groups 1000000 --steps 40 --also 3000:3020
       step prof_s8 300 python -u scripts/step_profile.py --groups 125000 --steps 40 --also 3000:3020
       ;;
+  fin)  # final verification of the committed tree: the GPU suite, smoke, the driver's command and the
+      # default (every leg, CPU baseline included), the 1/8 shard with the one-rank RCCL all-reduce
+      step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      step bench_driver 600 python -u bench.py --steps 20 --warmup 5
+      step bench_default 900 python -u bench.py
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step shard 300 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      summ $OUT/bench_*.log $OUT/shard.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
