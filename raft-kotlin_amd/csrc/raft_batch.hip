@@ -373,7 +373,13 @@ __global__ __launch_bounds__(NT) void bucket_batch_kernel(DevParams p, uint32_t 
     __shared__ uint32_t spos[GATHER_TILES], soff[GATHER_TILES];
     // a message outside the engine (bucket_tile_kernel): nothing is applied
     const bool bad = *(volatile unsigned int*)&dflags[0] != 0u;         // the same for the whole grid
-    const int bk = blockIdx.x;
+    // XCD-aware: workgroups b and b + 8 share an XCD (dealt round-robin), so
+    // XCD b % 8 takes the contiguous buckets [(b % 8) * C, (b % 8 + 1) * C) in
+    // order; neighbouring buckets share the 64-B lines of each tile's segment
+    // row and of its partitioned messages, which then come from one L2
+    const int xcb = (NB + 7) >> 3;
+    const int bk = (int)(blockIdx.x & 7u) * xcb + (int)(blockIdx.x >> 3);
+    if (bk >= NB) return;                                               // (the grid rounds NB up to 8 * C)
     const uint32_t kb = (uint32_t)bk << S;
     // this thread's tiles [tt0, tt1): their segments of this bucket, and
     // where they start in the bucket's batch order
@@ -545,7 +551,7 @@ static int run_batch_buckets(raft_engine* e, int kind, const int64_t* group, con
     bucket_tile_kernel<<<ntile, TILE_THREADS, tile_lds, e->stream>>>(
         group, dst, n, e->p.G, e->p.R, S, NB, bbits, tiles, seg, dflags, hflags);
     const BK kern = bucket_kernel_of(kind, e->p.mode == RAFT_MODE_TEXTBOOK);
-    kern<<<NB, BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, dflags,
+    kern<<<8 * ((NB + 7) >> 3), BUCKET_THREADS, 0, e->stream>>>(e->dp, (uint32_t)e->t, n, S, NB, ntile, tiles, seg, req, resp, dflags,
                                                hflags);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(e->stream));

@@ -383,6 +383,22 @@ case $P in
       RAFT_BENCH_FORCE_COLLECTIVE=1 step shard 300 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
       summ $OUT/bench_*.log $OUT/shard.log > $OUT/summary.txt
       ;;
+  xcd) # XCD-aware bucket order in bucket_batch_kernel (XCD b % 8 takes a contiguous bucket range, so
+      # neighbouring buckets share L2 lines of the segment table and the partitioned tiles): the batch
+      # tests, then the handler leg against the previous library (rev HEAD), interleaved; its PMC rows
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 \
+          --timeout-method thread -k "batch or handler or service or wire"
+      for i in 1 2 3; do
+        step new_$i 300 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_$i 300 python -u bench.py $H
+      done
+      for f in $OUT/new_*.log $OUT/prev_*.log; do
+        python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['handler_batch']; print(sys.argv[1].split('/')[-1], d['vote']['messages_per_s_device'], d['append']['messages_per_s_device'])" $f
+      done > $OUT/summary.txt
+      TAG=r6_xcd step pmch 900 bash scripts/pmc_handler.sh
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
