@@ -399,6 +399,48 @@ case $P in
       done > $OUT/summary.txt
       TAG=r6_xcd step pmch 900 bash scripts/pmc_handler.sh
       ;;
+  occ) # the handler kernel's occupancy: bucket_batch_kernel at amdgpu_waves_per_eu 8 (vote: 61 VGPRs, 4
+      # workgroups per CU instead of 3) and 6 / 8 (append: 80 VGPRs with 5 spills / 64 with 25; 3 or 4
+      # workgroups instead of 2) against production; the batch tests on each variant first
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      for v in w86 w88; do
+        RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step pytest_$v 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x \
+            -v --timeout 300 --timeout-method thread -k "batch or handler or service or wire"
+      done
+      for i in 1 2 3; do
+        step prod_$i 300 python -u bench.py $H
+        for v in w86 w88; do RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step ${v}_$i 300 python -u bench.py $H; done
+      done
+      for f in $OUT/prod_*.log $OUT/w8*.log; do
+        python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['handler_batch']; print(sys.argv[1].split('/')[-1], d['vote']['messages_per_s_device'], d['append']['messages_per_s_device'], d['vote']['parity_mismatches'], d['append']['parity_mismatches'])" $f
+      done > $OUT/summary.txt
+      ;;
+  pre) # append requests loaded before the handler kernel's LDS sort (in flight across it) and staged in
+      # LDS, the run's log[prev] read with the replica's fields; the vote kernel at 8 waves per SIMD: the
+      # batch tests, then the handler leg against the previous library (rev HEAD), interleaved
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 \
+          --timeout-method thread -k "batch or handler or service or wire"
+      for i in 1 2 3; do
+        step new_$i 300 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_prev.so step prev_$i 300 python -u bench.py $H
+      done
+      for f in $OUT/new_*.log $OUT/prev_*.log; do
+        python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['handler_batch']; print(sys.argv[1].split('/')[-1], d['vote']['messages_per_s_device'], d['append']['messages_per_s_device'], d['vote']['parity_mismatches'], d['append']['parity_mismatches'])" $f
+      done > $OUT/summary.txt
+      TAG=r6_pre step pmch 900 bash scripts/pmc_handler.sh
+      ;;
+  fin2) # final verification after the handler changes (XCD-aware bucket order, the vote kernel at 8 waves
+      # per SIMD): the handler PMC rows of this build, then the GPU suite, smoke and both bench commands
+      TAG=r6_fin2 step pmch 900 bash scripts/pmc_handler.sh
+      step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      step bench_driver 600 python -u bench.py --steps 20 --warmup 5
+      step bench_default 900 python -u bench.py
+      summ $OUT/bench_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
