@@ -441,6 +441,23 @@ case $P in
       step bench_default 900 python -u bench.py
       summ $OUT/bench_*.log > $OUT/summary.txt
       ;;
+  tiles) # tile shapes again after the XCD-aware bucket order (each bucket's segment-table and message
+      # lines now come through one L2, so more, smaller tiles cost the handler kernel less): 512 x 4 and
+      # 1024 x 4 against production's 512 x 8, interleaved, after the batch tests on each
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      for v in t512x4 t1024x4; do
+        RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step pytest_$v 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x \
+            -v --timeout 300 --timeout-method thread -k "batch or handler or service or wire"
+      done
+      for i in 1 2 3; do
+        step prod_$i 300 python -u bench.py $H
+        for v in t512x4 t1024x4; do RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step ${v}_$i 300 python -u bench.py $H; done
+      done
+      for f in $OUT/prod_*.log $OUT/t*.log; do
+        python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['handler_batch']; print(sys.argv[1].split('/')[-1], d['vote']['messages_per_s_device'], d['append']['messages_per_s_device'], d['vote']['parity_mismatches'], d['append']['parity_mismatches'])" $f
+      done > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
