@@ -458,6 +458,15 @@ case $P in
         python -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]['handler_batch']; print(sys.argv[1].split('/')[-1], d['vote']['messages_per_s_device'], d['append']['messages_per_s_device'], d['vote']['parity_mismatches'], d['append']['parity_mismatches'])" $f
       done > $OUT/summary.txt
       ;;
+  bands) # priority bands on the default's one launch of 400-step epochs (each epoch restarts the bands):
+      # e0 no age shifts, e1 later band ends 600/800/930, e3 earlier 400/700/880, against production
+      L=$PWD/raft-kotlin_amd/lib
+      for i in 1 2; do
+        step prod_def_$i 300 python -u bench.py $Q
+        for v in e0 e1 e3; do RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step ${v}_def_$i 300 python -u bench.py $Q; done
+      done
+      summ $OUT/*_def_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
