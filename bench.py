@@ -359,8 +359,7 @@ def parse_args(argv=None):
     ap.add_argument("--plan-only", action="store_true",
                     help="no GPU: start the ranks, agree on the shards over gloo, print them (tests)")
     args = ap.parse_args(argv)
-    if args.groups is None:
-        args.groups = abi.CONFIGS[args.config]["G"]
+    args.groups = abi.CONFIGS[args.config]["G"] if args.groups is None else args.groups
     return args
 
 
@@ -370,8 +369,7 @@ def rehearsal_count(rehearse_ms, groups, steps, coll=False, dev="cpu"):
     the same number of the repeats' collectives (tests/test_dist_cpu.py)."""
     n = max(1, math.ceil(rehearse_ms / 1e3 * REHEARSE_RATE / max(1, groups * steps)))
     if coll:
-        import torch
-        import torch.distributed as dist
+        import torch, torch.distributed as dist  # noqa: E401
         t = torch.tensor([n], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n = int(t.item())
