@@ -230,6 +230,39 @@ def test_steps_per_launch_invariance():
     assert all(d == digests[0] for d in digests)
 
 
+@pytest.mark.parametrize("variant", ["ring", "general", "textbook", "partitions"])
+def test_long_launch_kernel_variants(variant):
+    """A forced-balanced launch of 700 steps (steps_per_launch 1,000): the ring
+    and the general kernel run it as one launch of 400-step epochs; textbook
+    mode and a partitions-only workload have no epochs kernel, so it is cut
+    into 512 + 188.  Counters and digest equal 100-step launches, with kernel
+    timing on for the long runs."""
+    kw = dict(abi.CONFIGS[3], G=5000, churn_ppm=10_000)
+    if variant == "ring":
+        kw.update(log_window=64)
+    elif variant == "textbook":
+        kw.update(mode=abi.MODE_TEXTBOOK)
+    elif variant == "partitions":
+        kw = dict(abi.CONFIGS[5], G=3000)
+    runs = []
+    for k in (100, 1000):
+        e = RaftEngine(abi.make_params(log_cap=2000, steps_per_launch=k, schedule=abi.SCHED_BALANCED, **kw))
+        if variant == "general":
+            e.set_kernel(abi.KERNEL_GENERAL)
+        if k == 1000:
+            e.set_kernel_timing(True)
+        c = e.step(700)
+        info = e.kernel_info()
+        assert info["balanced"] >= 1
+        if k == 1000:
+            epochs = variant in ("ring", "general")
+            assert info["steps"] == (700 if epochs else 188), info
+            ms, launches = e.kernel_time()
+            assert launches == (1 if epochs else 2) and ms > 0
+        runs.append((e.digest(), c.tobytes()))
+    assert runs[0] == runs[1]
+
+
 def test_subrange_invariance():
     """Launch sub-ranges (raft_params.subranges: the grid split over 1-4
     streams, launches of different ranges overlapping, counter partials
