@@ -467,6 +467,15 @@ case $P in
       done
       summ $OUT/*_def_*.log > $OUT/summary.txt
       ;;
+  fin3) # the committed final tree: the GPU suite (C host and long-launch variants included), smoke, both
+      # bench commands and the 1/8 shard with the one-rank RCCL all-reduce
+      step pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+      step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()"
+      step bench_driver 600 python -u bench.py --steps 20 --warmup 5
+      step bench_default 900 python -u bench.py
+      RAFT_BENCH_FORCE_COLLECTIVE=1 step shard 300 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+      summ $OUT/bench_*.log $OUT/shard.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
