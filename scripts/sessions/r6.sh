@@ -476,6 +476,16 @@ case $P in
       RAFT_BENCH_FORCE_COLLECTIVE=1 step shard 300 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
       summ $OUT/bench_*.log $OUT/shard.log > $OUT/summary.txt
       ;;
+  swg) # the 1/8 shard's 20 steps with fewer balanced workgroups (schedule_workgroups 1,536 / 1,280: 6 / 5
+      # per CU, more chunk-steps per wave) against the resident 1,792, interleaved; the one-rank all-reduce
+      for i in 1 2 3; do
+        for w in 0 1536 1280; do
+          RAFT_BENCH_FORCE_COLLECTIVE=1 step s8_w${w}_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 \
+              --schedule-workgroups $w $Q
+        done
+      done
+      summ $OUT/s8_*.log > $OUT/summary.txt
+      ;;
   *) echo "unknown preset $P"; exit 2 ;;
 esac
 exit 0
