@@ -399,6 +399,18 @@ case $P in
       done > $OUT/summary.txt
       TAG=r6_xcd step pmch 900 bash scripts/pmc_handler.sh
       ;;
+  spec) # the append handler's first log[prev] fetched beside the replica's fields (production) against
+      # the previous tree (libraft_engine_base.so; not adopted, scripts/variants/append_prev_prefetch.patch): the batch tests on production, then 3 interleaved runs
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      step pytest 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+          -k "batch or handler or service or wire"
+      for i in 1 2 3; do
+        step prod_$i 300 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_base.so step base_$i 300 python -u bench.py $H
+      done
+      grep -ho '"handler_batch": {[^}]*' $OUT/prod_*.log $OUT/base_*.log > $OUT/summary.txt || true
+      ;;
   occ) # the handler kernel's occupancy: bucket_batch_kernel at amdgpu_waves_per_eu 8 (vote: 61 VGPRs, 4
       # workgroups per CU instead of 3) and 6 / 8 (append: 80 VGPRs with 5 spills / 64 with 25; 3 or 4
       # workgroups instead of 2) against production; the batch tests on each variant first
