@@ -411,6 +411,30 @@ case $P in
       done
       grep -ho '"handler_batch": {[^}]*' $OUT/prod_*.log $OUT/base_*.log > $OUT/summary.txt || true
       ;;
+  rmaj) # the state as one 64-B record per replica (scripts/variants/replica_major_state.patch: a handler's
+      # quads in one 64-B fetch; the step kernel's field loads 64 B apart per lane): the GPU suite on the
+      # variant, then production / variant interleaved on the driver's command + handler leg, the default
+      # and the 1/8 shard
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      RAFT_ENGINE_LIB=$L/libraft_engine_rmaj.so step pytest 600 python -u -m pytest tests -m gpu -x -v --timeout 300 \
+          --timeout-method thread
+      for i in 1 2 3; do
+        step prod_h_$i 300 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_rmaj.so step rmaj_h_$i 300 python -u bench.py $H
+      done
+      for i in 1 2; do
+        step prod_def_$i 300 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_rmaj.so step rmaj_def_$i 300 python -u bench.py $Q
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step prod_s8_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_rmaj.so RAFT_BENCH_FORCE_COLLECTIVE=1 step rmaj_s8_$i 200 python -u bench.py \
+            --groups 125000 --steps 20 --warmup 5 $Q
+      done
+      summ $OUT/prod_*.log $OUT/rmaj_*.log > $OUT/summary.txt
+      for f in $OUT/prod_h_*.log $OUT/rmaj_h_*.log; do
+        echo "$(basename $f) $(grep -o '"messages_per_s_device": [0-9.e+]*' $f | tr '\n' ' ')"
+      done >> $OUT/summary.txt
+      ;;
   occ) # the handler kernel's occupancy: bucket_batch_kernel at amdgpu_waves_per_eu 8 (vote: 61 VGPRs, 4
       # workgroups per CU instead of 3) and 6 / 8 (append: 80 VGPRs with 5 spills / 64 with 25; 3 or 4
       # workgroups instead of 2) against production; the batch tests on each variant first
