@@ -435,6 +435,46 @@ case $P in
         echo "$(basename $f) $(grep -o '"messages_per_s_device": [0-9.e+]*' $f | tr '\n' ' ')"
       done >> $OUT/summary.txt
       ;;
+  sched) # LLVM's AMDGPU scheduling strategies on the step kernel (scripts/build_variants.sh "ilp:-mllvm
+      # -amdgpu-sched-strategy=max-ilp", "memc:... =max-memory-clause"): the full-size digests on each, then
+      # production / ilp / memc interleaved on the driver's command and the 1/8 shard
+      L=$PWD/raft-kotlin_amd/lib
+      for v in ilp memc; do
+        RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step pytest_$v 400 python -u -m pytest tests/test_gpu_parity.py -m gpu \
+            -x -v --timeout 300 --timeout-method thread -k "full_size_digest"
+      done
+      for i in 1 2 3; do
+        step prod_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        for v in ilp memc; do
+          RAFT_ENGINE_LIB=$L/libraft_engine_$v.so step ${v}_d20_$i 200 python -u bench.py --steps 20 --warmup 5 $Q
+        done
+      done
+      for i in 1 2; do
+        RAFT_BENCH_FORCE_COLLECTIVE=1 step prod_s8_$i 200 python -u bench.py --groups 125000 --steps 20 --warmup 5 $Q
+        for v in ilp memc; do
+          RAFT_ENGINE_LIB=$L/libraft_engine_$v.so RAFT_BENCH_FORCE_COLLECTIVE=1 step ${v}_s8_$i 200 python -u bench.py \
+              --groups 125000 --steps 20 --warmup 5 $Q
+        done
+      done
+      summ $OUT/prod_*.log $OUT/ilp_*.log $OUT/memc_*.log > $OUT/summary.txt
+      ;;
+  ilp) # max-ilp scheduling on the whole library: production / ilp interleaved on the driver's command with
+      # the handler leg, and on the default (one 10^4-step launch of epochs)
+      L=$PWD/raft-kotlin_amd/lib
+      H="--steps 20 --warmup 5 --no-cpu-baseline --no-general-leg --stream-steps 0"
+      for i in 1 2 3; do
+        step prod_h_$i 300 python -u bench.py $H
+        RAFT_ENGINE_LIB=$L/libraft_engine_ilp.so step ilp_h_$i 300 python -u bench.py $H
+      done
+      for i in 1 2; do
+        step prod_def_$i 300 python -u bench.py $Q
+        RAFT_ENGINE_LIB=$L/libraft_engine_ilp.so step ilp_def_$i 300 python -u bench.py $Q
+      done
+      summ $OUT/prod_*.log $OUT/ilp_*.log > $OUT/summary.txt
+      for f in $OUT/prod_h_*.log $OUT/ilp_h_*.log; do
+        echo "$(basename $f) $(grep -o '"messages_per_s_device": [0-9.e+]*' $f | tr '\n' ' ')"
+      done >> $OUT/summary.txt
+      ;;
   occ) # the handler kernel's occupancy: bucket_batch_kernel at amdgpu_waves_per_eu 8 (vote: 61 VGPRs, 4
       # workgroups per CU instead of 3) and 6 / 8 (append: 80 VGPRs with 5 spills / 64 with 25; 3 or 4
       # workgroups instead of 2) against production; the batch tests on each variant first
